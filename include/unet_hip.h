@@ -1,0 +1,210 @@
+/*
+ * unet_hip.h — C-ABI of the MI355X (gfx950) Attention-U-Net hot path.
+ *
+ * The drop-in boundary of this build.  The reference (seagochen/unet-segment-pytorch) is pure Python
+ * and has no FFI: its device work is implicit ATen calls made from `nn.Module.forward`s.  Each entry
+ * point below replaces one of those call sites (or a fused group of them); the reference line it
+ * replaces is cited on each declaration.  The Python host (`unet/_hip/lib.py`) binds this header
+ * with ctypes — see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers + sizes only.  Activations are NHWC (channels innermost), element type chosen by
+ *    `dtype` (UNET_F32 or UNET_BF16); BN statistics, gradients and parameters are fp32.
+ *  - `stream` is a hipStream_t passed as void* (0 = legacy default stream).  No entry point
+ *    synchronises, allocates, or reads device memory from the host.
+ *  - Every entry point returns 0 on success or a hipError_t / UNET_ERR_* code; unet_last_error()
+ *    returns a static message describing the last failure on the calling thread.
+ *  - Workspace sizes are queried with the matching *_workspace() call and allocated by the caller.
+ */
+#ifndef UNET_HIP_H
+#define UNET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { UNET_F32 = 0, UNET_BF16 = 1 };
+enum { UNET_ERR_ARG = 1001, UNET_ERR_UNSUPPORTED = 1002 };
+
+/* How a convolution input channel range is produced from a stored tensor ("virtual activation").
+ * The conv kernels apply these transforms while staging input tiles into LDS, so BN-apply, ReLU,
+ * max-pool, bilinear upsample, zero-pad and the attention multiply are never materialised. */
+enum {
+  UNET_SRC_PLAIN = 0,    /* x[n,h,w,c] as stored                                                  */
+  UNET_SRC_ACT = 1,      /* relu?(x*scale[c]+shift[c]) (train/eval BN apply + ReLU), optional gate  */
+  UNET_SRC_POOL_ACT = 2, /* max over 2x2 of ACT(x) at (2h+i, 2w+j)           — layers.py:56        */
+  UNET_SRC_UP_ACT = 3,   /* bilinear(align_corners) of ACT(x), placed with pad — layers.py:78,183  */
+  UNET_SRC_NCHW_F32 = 4, /* fp32 NCHW model input (no transform)             — unet.py:75/177    */
+  UNET_SRC_UP_PLAIN = 5  /* PLAIN placed with pad offsets (ConvTranspose2d output, layers.py:101)  */
+};
+
+typedef struct unet_src {
+  int kind;             /* UNET_SRC_*                                                            */
+  int C;                /* channels contributed by this source                                   */
+  int H, W;             /* stored tensor spatial size                                            */
+  const void* data;     /* stored tensor (op dtype; fp32 for NCHW_F32)                           */
+  const float* scale;   /* ACT kinds: per-channel scale (gamma*invstd)                           */
+  const float* shift;   /* ACT kinds: per-channel shift (beta-mean*scale)                        */
+  int relu;             /* ACT kinds: apply ReLU after the affine                                */
+  int up_h, up_w;       /* UP kinds: interpolated size (before pad) / placed size for UP_PLAIN   */
+  int pad_t, pad_l;     /* UP kinds: placement of the interpolated map in the conv input         */
+  float sh, sw;         /* UP_ACT: align_corners source scales (H-1)/(up_h-1), (W-1)/(up_w-1)   */
+  const float* gate_p;  /* ACT only, optional: psi pre-activation p[n,h,w]; value *= sigmoid(...)  */
+  const float* gate_ab; /* ACT only: psi BN affine {scale, shift} (2 floats, device)              */
+} unet_src;
+
+/* Output modes of the implicit-GEMM convolution */
+enum {
+  UNET_OUT_Y = 0,         /* store y (op dtype, NHWC) + per-tile BN partial sums                  */
+  UNET_OUT_F32 = 1,       /* fp32 NHWC; split channels [0,split) -> out, [split,Cout) -> out2      */
+  UNET_OUT_POOL_BWD = 2   /* route to the 2x2 argmax of pool_src (ACT), add into out (fp32)        */
+};
+
+typedef struct unet_conv_desc {
+  int dtype;              /* UNET_F32 / UNET_BF16 — operand type of x/weights                     */
+  int N, H, W;            /* conv input == output spatial size (stride 1, 'same' padding)        */
+  int Cin, Cout;
+  int ksize;              /* 1 or 3                                                               */
+  int nsrc;               /* 1 or 2 (channel concat, src[0] first — layers.py:105,254)            */
+  unet_src src[2];
+  const void* weight;     /* packed by unet_pack_weight: [Cout][ksize^2][Cin_pad]                 */
+  int out_mode;           /* UNET_OUT_*                                                           */
+  void* out;              /* Y: op dtype [N,H,W,Cout]; F32: fp32 [N,H,W,split]                     */
+  void* out2;             /* F32 split: fp32 [N,H,W,Cout-split]                                   */
+  int split;              /* F32: channel split point (== Cout for no split)                       */
+  int accum, accum2;      /* F32: add into out / out2 instead of storing                          */
+  float* stats;           /* Y: [2][mtiles][Cout] partial sum / sum of squares (may be NULL)       */
+  unet_src pool_src;      /* POOL_BWD: the pre-pool activation (kind ACT, H=2H', W=2W')           */
+} unet_conv_desc;
+
+typedef struct unet_wgrad_desc {
+  int dtype;
+  int N, H, W, Cin, Cout, ksize, nsrc;
+  unet_src src[2];        /* conv input, same description as the forward                          */
+  const void* dy;         /* op dtype NHWC [N,H,W,Cout] — gradient at the conv output             */
+  float* dw;              /* fp32 OIHW [Cout][Cin][k][k] — output (overwritten, or += if accum)     */
+  int accum;
+  void* workspace;        /* unet_wgrad_workspace() bytes                                          */
+} unet_wgrad_desc;
+
+/* ---- misc ---------------------------------------------------------------------------------- */
+const char* unet_last_error(void);
+int unet_version(void);
+/* number of M tiles (8x16 output pixels) of a conv with this geometry: rows of the stats buffer  */
+int unet_conv_mtiles(int N, int H, int W);
+
+/* ---- weights (nn.Conv2d weight OIHW fp32 -> packed operand) -------------------------------- */
+/* replaces the implicit weight read of nn.Conv2d — layers.py:32,35,120,152,158,164            */
+/* transpose=0: [Cout][k*k][Cin_pad] ; transpose=1 (dgrad): [Cin][k*k (flipped)][Cout_pad]      */
+int unet_pack_weight(int dtype, const float* w_oihw, void* packed, int Cout, int Cin, int ksize,
+                     int transpose, void* stream);
+int unet_packed_weight_elems(int dtype, int Cout, int Cin, int ksize, int transpose);
+
+/* ---- convolution (fwd / dgrad) ------------------------------------------------------------- */
+/* replaces nn.Conv2d.forward (3x3 pad1 / 1x1, no bias) on a transformed input — layers.py:31-38,
+ * 55-58, 95-106, 151-160, 183-188, 241-255; and its input-gradient (convolution_backward dgrad) */
+int unet_conv(const unet_conv_desc* d, void* stream);
+
+/* ---- convolution weight gradient ----------------------------------------------------------- */
+size_t unet_wgrad_workspace(const unet_wgrad_desc* d);
+int unet_conv_wgrad(const unet_wgrad_desc* d, void* stream);
+
+/* ---- BatchNorm2d (train: batch stats; eval: running stats) — layers.py:33,36,153,159,165 ---- */
+/* reduce conv partial sums -> mean/invstd/scale/shift; update running stats in place (momentum<0:
+ * cumulative average as nn.BatchNorm2d(momentum=None)); ++num_batches_tracked                    */
+int unet_bn_finalize(const float* stats, int rows, int C, long long count, const float* gamma,
+                     const float* beta, float* running_mean, float* running_var,
+                     long long* num_batches_tracked, float momentum, float eps,
+                     float* mean, float* invstd, float* scale, float* shift, void* stream);
+int unet_bn_eval_affine(int C, const float* gamma, const float* beta, const float* running_mean,
+                        const float* running_var, float eps, float* scale, float* shift, void* stream);
+/* backward: g = da * [scale*y+shift > 0] (relu!=0) ; partial sums of g and g*xhat              */
+int unet_bn_bwd_reduce_rows(long long P, int C);
+int unet_bn_bwd_reduce(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
+                       const float* shift, int relu, const float* mean, const float* invstd,
+                       float* partial, void* stream);
+/* -> dgamma, dbeta (fp32 [C], stored or accumulated) and coef[3][C] with dy = A*g + B*y + Cc    */
+int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
+                         const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                         float* dbeta, int accum, float* coef, void* stream);
+/* column sums of a [rows][C] fp32 partial table (fp64 accumulation): out (+)= sum_r part[r][:]    */
+int unet_colsum(const float* part, int rows, int C, float* out, int accum, void* stream);
+/* dy (op dtype) = A*g + B*y + Cc                                                                */
+int unet_bn_bwd_apply(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
+                      const float* shift, int relu, const float* coef, void* dy, void* stream);
+
+/* ---- attention gate (AttentionGate.forward/backward) — layers.py:171-192 ---------------------- */
+/* p = sum_c wpsi_c * relu(sg*gw+bg + sx*xw+bx) ; partial sums of p                               */
+int unet_gate_psi_rows(long long P);
+int unet_gate_psi(int dtype, long long P, int Ci, const void* gw, const void* xw, const float* gab,
+                  const float* xab, const float* wpsi, float* p, float* partial, void* stream);
+/* backward 1: x = ACT(y_x); s = sigmoid(psi BN(p)); ds = sum_c d_c x_c; dx (+)= d*s; dq = ds s (1-s) */
+int unet_gate_bwd1(int dtype, long long P, int Cx, const float* dxs, const void* yx, const float* sx,
+                   const float* bx, int relu, const float* p, const float* psi_ab, const float* psi_mean,
+                   const float* psi_invstd, float* dx, int dx_accum, float* dq, float* partial, void* stream);
+/* backward 2 (reduce): dz = dp*wpsi*[a>0]; partial sums (dz, dz*ghat, dz*xhat, dp*a)             */
+int unet_gate_bwd2_rows(long long P, int Ci);
+int unet_gate_bwd2(int dtype, long long P, int Ci, const void* gw, const void* xw, const float* gab,
+                   const float* xab, const float* g_mean, const float* g_invstd, const float* x_mean,
+                   const float* x_invstd, const float* wpsi, const float* dq, const float* p,
+                   const float* psi_coef, float* partial, void* stream);
+/* finalize of bwd2: two unet_bn_bwd_finalize calls (partial rows 0/1 and 0/2) + unet_colsum (row 3)  */
+/* backward 3 (apply): dgw, dxw (op dtype)                                                        */
+int unet_gate_bwd3(int dtype, long long P, int Ci, const void* gw, const void* xw, const float* gab,
+                   const float* xab, const float* wpsi, const float* dq, const float* p,
+                   const float* psi_coef, const float* gcoef, const float* xcoef, void* dgw, void* dxw,
+                   void* stream);
+
+/* ---- bilinear resampling (align_corners=True) — layers.py:78,183 ; unet.py:206-208 ---------- */
+/* backward of UP: gather-form adjoint of the interpolation (deterministic).  d_up is fp32 NHWC
+ * [N,Hp,Wp,C] (the padded map), result fp32 NHWC [N,Hs,Ws,C] stored or accumulated             */
+int unet_upsample_bwd(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pad_t, int pad_l,
+                      int Hp, int Wp, float sh, float sw, const float* d_up, float* dx, int accum,
+                      void* stream);
+/* generic fp32 NCHW bilinear resize (deep-supervision heads) fwd and bwd                         */
+int unet_resize_nchw(long long NC, int Hi, int Wi, int Ho, int Wo, float sh, float sw, const float* x,
+                     float* y, void* stream);
+int unet_resize_nchw_bwd(long long NC, int Hi, int Wi, int Ho, int Wo, float sh, float sw,
+                         const float* dy, float* dx, int accum, void* stream);
+
+/* ---- OutConv (1x1 conv + bias, few classes) — layers.py:109-123 ------------------------------ */
+int unet_outconv_rows(long long P);
+int unet_outconv_fwd(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
+                     const float* shift, int relu, const float* w, const float* b, float* logits_nchw,
+                     void* stream);
+int unet_outconv_bwd(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
+                     const float* shift, int relu, const float* w, const float* dlogits_nchw, float* da,
+                     int da_accum, float* partial, void* stream);
+int unet_outconv_bwd_finalize(const float* partial, int rows, int C, int K, float* dw, float* db,
+                              int accum, void* stream);
+
+/* ---- layout ---------------------------------------------------------------------------------- */
+/* NCHW fp32 <-> NHWC (op dtype / fp32) for standalone module calls                                */
+int unet_nchw_to_nhwc(int dtype, long long N, int C, int H, int W, const float* x, void* y, void* stream);
+int unet_nhwc_to_nchw(int dtype, long long N, int C, int H, int W, const void* x, const float* scale,
+                      const float* shift, int relu, float* y, void* stream);
+/* x*sigmoid(psi BN(p)) of an ACT tensor as NCHW fp32 (standalone AttentionGate output)           */
+int unet_gated_to_nchw(int dtype, long long N, int C, int H, int W, const void* x, const float* scale,
+                       const float* shift, int relu, const float* p, const float* psi_ab, float* y, void* stream);
+int unet_fill_f32(float* x, long long n, float v, void* stream);
+
+/* ---- DiceBCE / Dice / BalancedCE loss + grad — loss.py:18-191 ------------------------------- */
+int unet_loss_rows(long long HW);
+/* pass 1: per-image partial sums (fp32 NCHW logits, int64 targets)                               */
+int unet_loss_reduce(long long N, int K, long long HW, const float* z, const int64_t* t, float* partial,
+                     void* stream);
+/* finalize: loss scalar(s) + per-(n,c) gradient coefficients                                    */
+int unet_loss_finalize(const float* partial, int rows, long long N, int K, float ce_w, float dice_w,
+                       float class_w, float ce_smooth, float dice_smooth, int ignore_bg, int reduction,
+                       float* loss, float* coef, void* stream);
+/* pass 2: dz = gout * d loss / dz                                                                 */
+int unet_loss_grad(long long N, int K, long long HW, const float* z, const int64_t* t, const float* coef,
+                   const float* gout, int gout_per_elem, int ignore_bg, float* dz, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNET_HIP_H */

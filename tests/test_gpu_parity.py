@@ -1,0 +1,118 @@
+"""GPU parity: the HIP path (through the C-ABI library) vs the golden fixtures recorded from the
+reference, and vs the CPU oracle.  fp32 operand mode must match to fp32 noise; bf16 mode within the
+bf16 tolerances of SURVEY.md §8(d)."""
+
+import pytest
+import torch
+
+from hip_helpers import build_model, grad_report, max_abs, rel_err
+
+pytestmark = pytest.mark.gpu
+
+MODULE_CASES = ["double_conv", "double_conv_mid", "down", "up_bilinear", "out_conv", "attention_gate",
+                "attention_gate_odd", "attention_up"]
+
+
+def _module_for(name, rec):
+    from unet.models import AttentionGate, AttentionUp, DoubleConv, Down, OutConv, Up
+    ctor = {
+        "double_conv": lambda: DoubleConv(16, 32),
+        "double_conv_mid": lambda: DoubleConv(24, 8, 12),
+        "down": lambda: Down(16, 32),
+        "up_bilinear": lambda: Up(32, 8, bilinear=True),
+        "up_transposed": lambda: Up(32, 16, bilinear=False),
+        "out_conv": lambda: OutConv(16, 2),
+        "attention_gate": lambda: AttentionGate(16, 16),
+        "attention_gate_odd": lambda: AttentionGate(16, 8, 4),
+        "attention_up": lambda: AttentionUp(32, 8, bilinear=True),
+        "attention_up_transposed": lambda: AttentionUp(32, 16, bilinear=False),
+    }[name]
+    m = ctor()
+    m.load_state_dict(rec["init"])
+    return m.cuda().train()
+
+
+@pytest.mark.parametrize("name", MODULE_CASES)
+def test_module_fp32_vs_golden(golden_modules, name):
+    rec = golden_modules[name]
+    m = _module_for(name, rec)
+    m.hip_precision = "fp32"
+    ins = [i.cuda().requires_grad_(True) for i in rec["inputs"]]
+    y = m(*ins)
+    (y * rec["gout"].cuda()).sum().backward()
+    assert max_abs(y, rec["out"]) <= 1e-4 * (1 + float(rec["out"].abs().max()))
+    for gi, ref in zip(ins, rec["grad_inputs"]):
+        assert max_abs(gi.grad, ref) <= 2e-4 * (1 + float(ref.abs().max())), name
+    e, k = grad_report(m, rec["grads"])
+    assert e <= 2e-4, (name, k, e)
+    for k, b in rec["buffers_after"].items():
+        mine = dict(m.named_buffers())[k]
+        assert max_abs(mine.float(), b.float()) <= 1e-4 * (1 + float(b.float().abs().max())), (name, k)
+
+
+MODEL_CASES = ["attention_unet_b8", "unet_b8", "attention_unet_b4_ds", "attention_unet_b4_odd"]
+
+
+@pytest.mark.parametrize("name", MODEL_CASES)
+def test_model_fp32_vs_golden(golden_models, name):
+    from unet.utils.loss import DeepSupervisionLoss, DiceBCELoss
+    rec = golden_models[name]
+    m = build_model(rec)
+    m.hip_precision = "fp32"
+    m.train()
+    x, t = rec["x"].cuda(), rec["t"].cuda()
+    out = m(x)
+    crit = DiceBCELoss()
+    if rec["deep_supervision"]:
+        crit = DeepSupervisionLoss(crit)
+    loss = crit(out, t)
+    loss.backward()
+    outs = out if isinstance(out, list) else [out]
+    for o, r in zip(outs, rec["outputs"]):
+        assert max_abs(o, r) <= 1e-4, name                       # logits within 1e-4 (north_star)
+    assert abs(float(loss) - float(rec["loss"])) <= 1e-5 * (1 + abs(float(rec["loss"])))
+    e, k = grad_report(m, rec["grads"])
+    assert e <= 1e-3, (name, k, e)
+    bufs = dict(m.named_buffers())
+    for k, b in rec["buffers_after"].items():
+        assert max_abs(bufs[k].float(), b.float()) <= 1e-4 * (1 + float(b.float().abs().max())), (name, k)
+    m.eval()
+    with torch.no_grad():
+        ev = m(x)
+    assert max_abs(ev, rec["eval_logits"]) <= 1e-4 * (1 + float(rec["eval_logits"].abs().max()))
+
+
+def test_model_bf16_vs_golden(golden_models):
+    from unet.utils.loss import DiceBCELoss
+    rec = golden_models["attention_unet_b8"]
+    m = build_model(rec)
+    m.hip_precision = "bf16"
+    out = m(rec["x"].cuda())
+    loss = DiceBCELoss()(out, rec["t"].cuda())
+    loss.backward()
+    assert rel_err(out, rec["outputs"][0]) <= 2e-2
+    assert abs(float(loss) - float(rec["loss"])) <= 2e-2 * abs(float(rec["loss"]))
+
+
+@pytest.mark.parametrize("name", ["dice_bce", "dice", "balanced_ce", "dice_bce_w"])
+def test_loss_vs_golden(golden_losses, name):
+    from unet.utils.loss import BalancedCELoss, DiceBCELoss, DiceLoss
+    crit = {"dice_bce": DiceBCELoss(), "dice": DiceLoss(), "balanced_ce": BalancedCELoss(),
+            "dice_bce_w": DiceBCELoss(ce_weight=0.7, dice_weight=1.3, class_weight=0.3)}[name]
+    z = golden_losses["z"].cuda().requires_grad_(True)
+    t = golden_losses["t"].cuda()
+    loss = crit(z, t)
+    loss.backward()
+    ref = golden_losses["cases"][name]
+    assert abs(float(loss) - float(ref["loss"])) <= 1e-5 * (1 + abs(float(ref["loss"])))
+    assert max_abs(z.grad, ref["grad"]) <= 1e-6 + 1e-4 * float(ref["grad"].abs().max())
+
+
+def test_loss_three_classes(golden_losses):
+    from unet.utils.loss import DiceBCELoss
+    ref = golden_losses["cases"]["dice_bce_c3"]
+    z = ref["z"].cuda().requires_grad_(True)
+    loss = DiceBCELoss()(z, ref["t"].cuda())
+    loss.backward()
+    assert abs(float(loss) - float(ref["loss"])) <= 1e-5 * (1 + abs(float(ref["loss"])))
+    assert max_abs(z.grad, ref["grad"]) <= 1e-6 + 1e-4 * float(ref["grad"].abs().max())

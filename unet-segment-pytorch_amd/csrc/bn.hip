@@ -1,0 +1,245 @@
+// bn.hip — training-mode BatchNorm2d statistics and backward for NHWC activations.
+//
+// Reference: nn.BatchNorm2d in unet/models/layers.py:33,36,153,159,165 (train mode: biased batch
+// variance to normalise, unbiased variance into running_var, momentum 0.1, eps 1e-5).  The forward
+// statistics come from the conv epilogue's per-tile partial sums; they are reduced here in a fixed
+// order in fp64 (deterministic, like the CPU path's double accumulation).  The backward is
+//   g    = da * [scale*y + shift > 0]                       (ReLU, layers.py:34,37)
+//   dβ   = Σ g,  dγ = Σ g·x̂,  dy = γ·invstd·(g − dβ/M − x̂·dγ/M)
+// as two streaming passes (reduce, apply) around a per-channel finalize.
+#include "common.h"
+
+namespace unet {
+
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((tid & 63) == 0) sh[tid >> 6] = v;
+  __syncthreads();
+  double r = 0;
+  if (tid == 0) {
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r += sh[w];
+    sh[0] = r;
+  }
+  __syncthreads();
+  r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// one block per channel
+__global__ void bn_finalize_kernel(const float* stats, int rows, int C, long long count, const float* gamma,
+                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
+                                   float eps, float* mean, float* invstd, float* scale, float* shift) {
+  __shared__ double sh[16];
+  const int c = blockIdx.x;
+  double s = 0, ss = 0;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+    s += stats[(size_t)r * C + c];
+    ss += stats[((size_t)rows + r) * C + c];
+  }
+  s = block_sum_d(s, sh);
+  ss = block_sum_d(ss, sh);
+  if (threadIdx.x == 0) {
+    const double m = s / (double)count;
+    double var = ss / (double)count - m * m;
+    if (var < 0) var = 0;
+    const double is = 1.0 / sqrt(var + (double)eps);
+    mean[c] = (float)m;
+    invstd[c] = (float)is;
+    const float sc = (float)((double)gamma[c] * is);
+    scale[c] = sc;
+    shift[c] = (float)((double)beta[c] - m * (double)gamma[c] * is);
+    if (rmean && rvar) {
+      double f = momentum;
+      if (momentum < 0) f = nbt ? 1.0 / (double)(*nbt + 1) : 1.0;  // momentum=None: cumulative average
+      const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+      rmean[c] = (float)((1.0 - f) * (double)rmean[c] + f * m);
+      rvar[c] = (float)((1.0 - f) * (double)rvar[c] + f * unb);
+    }
+    if (c == 0 && nbt) *nbt += 1;
+  }
+}
+
+__global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                               float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = 1.0f / sqrtf(rv[c] + eps);
+  const float sc = gamma[c] * is;
+  scale[c] = sc;
+  shift[c] = beta[c] - rm[c] * sc;
+}
+
+// 2-D layout: CL channel lanes x (256/CL) pixel rows; grid (ceil(C/CL), rows)
+static inline int chan_lanes(int C) {
+  int cl = 1;
+  while (cl < C && cl < 64) cl <<= 1;
+  return cl;
+}
+static inline int reduce_rows(long long P, int C) {
+  const int cl = chan_lanes(C);
+  const int cblocks = (C + cl - 1) / cl;
+  long long r = (2048 + cblocks - 1) / cblocks;
+  const long long maxr = (P + 63) / 64;  // at least 64 pixels per block
+  if (r > maxr) r = maxr;
+  if (r < 1) r = 1;
+  return (int)r;
+}
+
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(long long P, int C, int CL, const float* da, const T* y, const float* scale,
+                                     const float* shift, int relu, const float* mean, const float* invstd, float* part,
+                                     int rows) {
+  __shared__ float sh[2][256];
+  const int tid = threadIdx.x;
+  const int cx = tid % CL, py = tid / CL, R = blockDim.x / CL;
+  const int c = blockIdx.x * CL + cx;
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.y * per, p1 = min(P, p0 + per);
+  float sg = 0.f, sgx = 0.f;
+  if (c < C) {
+    const float sc = scale[c], sf = shift[c], mu = mean[c], is = invstd[c];
+    for (long long p = p0 + py; p < p1; p += R) {
+      const float yv = to_f(y[p * C + c]);
+      float g = da[p * C + c];
+      if (relu && !(yv * sc + sf > 0.f)) g = 0.f;
+      sg += g;
+      sgx += g * (yv - mu) * is;
+    }
+  }
+  sh[0][tid] = sg;
+  sh[1][tid] = sgx;
+  __syncthreads();
+  if (py == 0 && c < C) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < R; ++r) { a += sh[0][r * CL + cx]; b += sh[1][r * CL + cx]; }
+    part[(size_t)blockIdx.y * C + c] = a;
+    part[((size_t)rows + blockIdx.y) * C + c] = b;
+  }
+}
+
+// one block per channel: sums over rows in fp64
+__global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
+                                       const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                                       float* dbeta, int accum, float* coef) {
+  __shared__ double sh[16];
+  const int c = blockIdx.x;
+  double a = 0, b = 0;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+    a += sum_g[(size_t)r * C + c];
+    b += sum_gx[(size_t)r * C + c];
+  }
+  a = block_sum_d(a, sh);
+  b = block_sum_d(b, sh);
+  if (threadIdx.x == 0) {
+    if (dbeta) dbeta[c] = accum ? dbeta[c] + (float)a : (float)a;
+    if (dgamma) dgamma[c] = accum ? dgamma[c] + (float)b : (float)b;
+    if (coef) {
+      const double k = (double)gamma[c] * invstd[c];
+      const double M = (double)count;
+      const double B = -k * (double)invstd[c] * b / M;
+      coef[c] = (float)k;
+      coef[C + c] = (float)B;
+      coef[2 * C + c] = (float)(-k * a / M - B * (double)mean[c]);
+    }
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(long long P, int C, int CL, const float* da, const T* y, const float* scale,
+                                    const float* shift, int relu, const float* coef, T* dy, int rows) {
+  const int tid = threadIdx.x;
+  const int cx = tid % CL, py = tid / CL, R = blockDim.x / CL;
+  const int c = blockIdx.x * CL + cx;
+  if (c >= C) return;
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.y * per, p1 = min(P, p0 + per);
+  const float sc = scale[c], sf = shift[c], A = coef[c], B = coef[C + c], Cc = coef[2 * C + c];
+  for (long long p = p0 + py; p < p1; p += R) {
+    const float yv = to_f(y[p * C + c]);
+    float g = da[p * C + c];
+    if (relu && !(yv * sc + sf > 0.f)) g = 0.f;
+    dy[p * C + c] = from_f<T>(A * g + B * yv + Cc);
+  }
+}
+
+// column sums over rows (fp64): out[c] (+)= sum_r part[r][c]
+__global__ void colsum_kernel(const float* part, int rows, int C, float* out, int accum) {
+  __shared__ double sh[16];
+  const int c = blockIdx.x;
+  double a = 0;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) a += part[(size_t)r * C + c];
+  a = block_sum_d(a, sh);
+  if (threadIdx.x == 0) out[c] = accum ? out[c] + (float)a : (float)a;
+}
+
+}  // namespace unet
+
+using namespace unet;
+
+extern "C" {
+
+int unet_bn_finalize(const float* stats, int rows, int C, long long count, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, long long* nbt, float momentum, float eps, float* mean,
+                     float* invstd, float* scale, float* shift, void* stream) {
+  if (!stats || rows <= 0 || C <= 0 || count <= 0 || !gamma || !beta || !mean || !invstd || !scale || !shift) {
+    set_error("unet_bn_finalize: bad args");
+    return UNET_ERR_ARG;
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, stats, rows, C, count, gamma,
+                     beta, running_mean, running_var, nbt, momentum, eps, mean, invstd, scale, shift);
+  return check_launch("bn_finalize");
+}
+
+int unet_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                        float* scale, float* shift, void* stream) {
+  hipLaunchKernelGGL(bn_eval_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, C, gamma, beta, rm, rv,
+                     eps, scale, shift);
+  return check_launch("bn_eval_affine");
+}
+
+int unet_bn_bwd_reduce_rows(long long P, int C) { return reduce_rows(P, C); }
+
+int unet_bn_bwd_reduce(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
+                       const float* shift, int relu, const float* mean, const float* invstd, float* partial,
+                       void* stream) {
+  const int cl = chan_lanes(C), rows = reduce_rows(P, C);
+  dim3 grid(cdiv(C, cl), rows);
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, C, cl, da,
+                       (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, P, C, cl, da,
+                       (const float*)y, scale, shift, relu, mean, invstd, partial, rows);
+  return check_launch("bn_bwd_reduce");
+}
+
+int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int C, long long count, const float* gamma,
+                         const float* mean, const float* invstd, float* dgamma, float* dbeta, int accum, float* coef,
+                         void* stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, sum_g, sum_gx, rows, C, count,
+                     gamma, mean, invstd, dgamma, dbeta, accum, coef);
+  return check_launch("bn_bwd_finalize");
+}
+
+int unet_bn_bwd_apply(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
+                      const float* shift, int relu, const float* coef, void* dy, void* stream) {
+  const int cl = chan_lanes(C), rows = reduce_rows(P, C);
+  dim3 grid(cdiv(C, cl), rows);
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, C, cl, da,
+                       (const bf16*)y, scale, shift, relu, coef, (bf16*)dy, rows);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, P, C, cl, da,
+                       (const float*)y, scale, shift, relu, coef, (float*)dy, rows);
+  return check_launch("bn_bwd_apply");
+}
+
+int unet_colsum(const float* part, int rows, int C, float* out, int accum, void* stream) {
+  hipLaunchKernelGGL(colsum_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, part, rows, C, out, accum);
+  return check_launch("colsum");
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// common.h — shared device helpers for the gfx950 (CDNA4) Attention-U-Net kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "unet_hip.h"
+
+namespace unet {
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short i16x4;
+
+constexpr int WAVE = 64;
+
+// ------------------------------------------------------------------------------------------------
+// element traits: a 16-byte vector of T, conversions to/from float
+// ------------------------------------------------------------------------------------------------
+template <typename T> struct Vec;
+template <> struct Vec<float> {
+  static constexpr int N = 4;
+  typedef float4 type;
+};
+template <> struct Vec<bf16> {
+  static constexpr int N = 8;
+  typedef uint4 type;
+};
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// load VEC elements (16 B aligned) into floats
+template <typename T> __device__ __forceinline__ void load_vec(const T* p, float* v);
+template <> __device__ __forceinline__ void load_vec<float>(const float* p, float* v) {
+  float4 q = *reinterpret_cast<const float4*>(p);
+  v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+}
+template <> __device__ __forceinline__ void load_vec<bf16>(const bf16* p, float* v) {
+  uint4 q = *reinterpret_cast<const uint4*>(p);
+  unsigned u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(u[i] << 16);
+    v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+  }
+}
+template <typename T> __device__ __forceinline__ void store_vec(T* p, const float* v);
+template <> __device__ __forceinline__ void store_vec<float>(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> __device__ __forceinline__ void store_vec<bf16>(bf16* p, const float* v) {
+  bf16 b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = (bf16)v[i];
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(b);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// ------------------------------------------------------------------------------------------------
+// wave reductions (wave64)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// error plumbing
+// ------------------------------------------------------------------------------------------------
+void set_error(const char* msg);
+int check_launch(const char* what);
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace unet

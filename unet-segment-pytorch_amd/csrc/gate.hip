@@ -1,0 +1,244 @@
+// gate.hip — AttentionGate (unet/models/layers.py:126-192) element/reduction passes.
+//
+// Forward:  gw = W_g·g_up and xw = W_x·x are produced by the 1x1 conv kernel (with BN partials).
+//           psi pass (here): a = relu(bn_g(gw) + bn_x(xw)); p = wpsi·a; partial Σp, Σp²   (:186-189)
+//           s = sigmoid(bn_psi(p)) is never stored: the next conv's loader evaluates it (:192).
+// Backward: bwd1  (per pixel)   ds = Σ_c d(x·s)_c x_c ; dx (+)= d·s ; dq = ds·s(1−s) ; Σdq, Σdq·p̂
+//           bwd2  (per channel) dz = dp·wpsi·[a>0] ; Σdz, Σdz·ĝ, Σdz·x̂, Σdp·a
+//           bwd3  (apply)       dgw, dxw = BN-backward(dz)  -> 1x1 conv dgrad/wgrad
+#include "common.h"
+
+namespace unet {
+
+static inline int chan_lanes_g(int C) {
+  int cl = 1;
+  while (cl < C && cl < 64) cl <<= 1;
+  return cl;
+}
+static inline int rows_for(long long P, int C) {
+  const int cl = chan_lanes_g(C);
+  const int cblocks = (C + cl - 1) / cl;
+  long long r = (2048 + cblocks - 1) / cblocks;
+  const long long maxr = (P + 63) / 64;
+  if (r > maxr) r = maxr;
+  if (r < 1) r = 1;
+  return (int)r;
+}
+static inline int pix_rows(long long P) {
+  long long r = (P + 255) / 256;
+  if (r > 2048) r = 2048;
+  if (r < 1) r = 1;
+  return (int)r;
+}
+
+__device__ __forceinline__ float block_sum_f(float v, float* sh) {
+  const int tid = threadIdx.x;
+  v = wave_sum(v);
+  if ((tid & 63) == 0) sh[tid >> 6] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r += sh[w];
+  __syncthreads();
+  return r;
+}
+
+// one thread per pixel; grid-stride over a contiguous pixel range per block (deterministic partials)
+template <typename T>
+__global__ void psi_kernel(long long P, int Ci, const T* gw, const T* xw, const float* gab, const float* xab,
+                           const float* wpsi, float* p, float* part, int rows) {
+  __shared__ float sh[8];
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  float s = 0.f, ss = 0.f;
+  for (long long q = p0 + threadIdx.x; q < p1; q += blockDim.x) {
+    const T* g = gw + q * Ci;
+    const T* x = xw + q * Ci;
+    float acc = 0.f;
+    for (int c = 0; c < Ci; ++c) {
+      const float a = fmaxf(to_f(g[c]) * gab[c] + gab[Ci + c] + to_f(x[c]) * xab[c] + xab[Ci + c], 0.f);
+      acc += wpsi[c] * a;
+    }
+    p[q] = acc;
+    s += acc;
+    ss += acc * acc;
+  }
+  s = block_sum_f(s, sh);
+  ss = block_sum_f(ss, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s;
+    part[rows + blockIdx.x] = ss;
+  }
+}
+
+template <typename T>
+__global__ void gate_bwd1_kernel(long long P, int Cx, const float* dxs, const T* yx, const float* sx, const float* bx,
+                                 int relu, const float* pp, const float* psi_ab, const float* psi_mean,
+                                 const float* psi_inv, float* dx, int dx_accum, float* dq, float* part, int rows) {
+  __shared__ float sh[8];
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  const float pa = psi_ab[0], pb = psi_ab[1], pm = psi_mean[0], pi = psi_inv[0];
+  float s1 = 0.f, s2 = 0.f;
+  for (long long q = p0 + threadIdx.x; q < p1; q += blockDim.x) {
+    const float pv = pp[q];
+    const float sg = sigmoidf_(pv * pa + pb);
+    const float* d = dxs + q * Cx;
+    const T* y = yx + q * Cx;
+    float* o = dx + q * Cx;
+    float ds = 0.f;
+    for (int c = 0; c < Cx; ++c) {
+      float xv = to_f(y[c]) * sx[c] + bx[c];
+      if (relu) xv = fmaxf(xv, 0.f);
+      const float dv = d[c];
+      ds += dv * xv;
+      const float g = dv * sg;
+      o[c] = dx_accum ? o[c] + g : g;
+    }
+    const float dqv = ds * sg * (1.f - sg);
+    dq[q] = dqv;
+    s1 += dqv;
+    s2 += dqv * (pv - pm) * pi;
+  }
+  s1 = block_sum_f(s1, sh);
+  s2 = block_sum_f(s2, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s1;
+    part[rows + blockIdx.x] = s2;
+  }
+}
+
+// channel lanes x pixel rows
+template <typename T>
+__global__ void gate_bwd2_kernel(long long P, int Ci, int CL, const T* gw, const T* xw, const float* gab,
+                                 const float* xab, const float* gm, const float* gi, const float* xm, const float* xi,
+                                 const float* wpsi, const float* dq, const float* pp, const float* pc, float* part,
+                                 int rows) {
+  __shared__ float sh[4][256];
+  const int tid = threadIdx.x;
+  const int cx = tid % CL, py = tid / CL, R = blockDim.x / CL;
+  const int c = blockIdx.x * CL + cx;
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.y * per, p1 = min(P, p0 + per);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < Ci) {
+    const float gs = gab[c], gb = gab[Ci + c], xs = xab[c], xb = xab[Ci + c];
+    const float gmu = gm[c], giv = gi[c], xmu = xm[c], xiv = xi[c], w = wpsi[c];
+    const float A = pc[0], B = pc[1], Cc = pc[2];
+    for (long long q = p0 + py; q < p1; q += R) {
+      const float g = to_f(gw[q * Ci + c]), x = to_f(xw[q * Ci + c]);
+      const float a = fmaxf(g * gs + gb + x * xs + xb, 0.f);
+      const float dp = A * dq[q] + B * pp[q] + Cc;
+      const float dz = a > 0.f ? dp * w : 0.f;
+      a0 += dz;
+      a1 += dz * (g - gmu) * giv;
+      a2 += dz * (x - xmu) * xiv;
+      a3 += dp * a;
+    }
+  }
+  sh[0][tid] = a0;
+  sh[1][tid] = a1;
+  sh[2][tid] = a2;
+  sh[3][tid] = a3;
+  __syncthreads();
+  if (py == 0 && c < Ci) {
+    float r[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) r[f] += sh[f][k * CL + cx];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) part[((size_t)f * rows + blockIdx.y) * Ci + c] = r[f];
+  }
+}
+
+template <typename T>
+__global__ void gate_bwd3_kernel(long long P, int Ci, int CL, const T* gw, const T* xw, const float* gab,
+                                 const float* xab, const float* wpsi, const float* dq, const float* pp, const float* pc,
+                                 const float* gcoef, const float* xcoef, T* dgw, T* dxw, int rows) {
+  const int tid = threadIdx.x;
+  const int cx = tid % CL, py = tid / CL, R = blockDim.x / CL;
+  const int c = blockIdx.x * CL + cx;
+  if (c >= Ci) return;
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.y * per, p1 = min(P, p0 + per);
+  const float gs = gab[c], gb = gab[Ci + c], xs = xab[c], xb = xab[Ci + c], w = wpsi[c];
+  const float A = pc[0], B = pc[1], Cc = pc[2];
+  const float gA = gcoef[c], gB = gcoef[Ci + c], gC = gcoef[2 * Ci + c];
+  const float xA = xcoef[c], xB = xcoef[Ci + c], xC = xcoef[2 * Ci + c];
+  for (long long q = p0 + py; q < p1; q += R) {
+    const float g = to_f(gw[q * Ci + c]), x = to_f(xw[q * Ci + c]);
+    const float a = fmaxf(g * gs + gb + x * xs + xb, 0.f);
+    const float dp = A * dq[q] + B * pp[q] + Cc;
+    const float dz = a > 0.f ? dp * w : 0.f;
+    dgw[q * Ci + c] = from_f<T>(gA * dz + gB * g + gC);
+    dxw[q * Ci + c] = from_f<T>(xA * dz + xB * x + xC);
+  }
+}
+
+}  // namespace unet
+
+using namespace unet;
+
+extern "C" {
+
+int unet_gate_psi_rows(long long P) { return pix_rows(P); }
+
+int unet_gate_psi(int dtype, long long P, int Ci, const void* gw, const void* xw, const float* gab, const float* xab,
+                  const float* wpsi, float* p, float* partial, void* stream) {
+  const int rows = pix_rows(P);
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(psi_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, (const bf16*)gw,
+                       (const bf16*)xw, gab, xab, wpsi, p, partial, rows);
+  else
+    hipLaunchKernelGGL(psi_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, (const float*)gw,
+                       (const float*)xw, gab, xab, wpsi, p, partial, rows);
+  return check_launch("gate_psi");
+}
+
+int unet_gate_bwd1(int dtype, long long P, int Cx, const float* dxs, const void* yx, const float* sx, const float* bx,
+                   int relu, const float* p, const float* psi_ab, const float* psi_mean, const float* psi_invstd, float* dx,
+                   int dx_accum, float* dq, float* partial, void* stream) {
+  const int rows = pix_rows(P);
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(gate_bwd1_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, dxs,
+                       (const bf16*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial, rows);
+  else
+    hipLaunchKernelGGL(gate_bwd1_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, dxs,
+                       (const float*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial, rows);
+  return check_launch("gate_bwd1");
+}
+
+int unet_gate_bwd2_rows(long long P, int Ci) { return rows_for(P, Ci); }
+
+int unet_gate_bwd2(int dtype, long long P, int Ci, const void* gw, const void* xw, const float* gab, const float* xab,
+                   const float* g_mean, const float* g_invstd, const float* x_mean, const float* x_invstd,
+                   const float* wpsi, const float* dq, const float* p, const float* psi_coef, float* partial,
+                   void* stream) {
+  const int cl = chan_lanes_g(Ci), rows = rows_for(P, Ci);
+  dim3 grid(cdiv(Ci, cl), rows);
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(gate_bwd2_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const bf16*)gw,
+                       (const bf16*)xw, gab, xab, g_mean, g_invstd, x_mean, x_invstd, wpsi, dq, p, psi_coef, partial,
+                       rows);
+  else
+    hipLaunchKernelGGL(gate_bwd2_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const float*)gw,
+                       (const float*)xw, gab, xab, g_mean, g_invstd, x_mean, x_invstd, wpsi, dq, p, psi_coef, partial,
+                       rows);
+  return check_launch("gate_bwd2");
+}
+
+int unet_gate_bwd3(int dtype, long long P, int Ci, const void* gw, const void* xw, const float* gab, const float* xab,
+                   const float* wpsi, const float* dq, const float* p, const float* psi_coef, const float* gcoef,
+                   const float* xcoef, void* dgw, void* dxw, void* stream) {
+  const int cl = chan_lanes_g(Ci), rows = rows_for(P, Ci);
+  dim3 grid(cdiv(Ci, cl), rows);
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(gate_bwd3_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const bf16*)gw,
+                       (const bf16*)xw, gab, xab, wpsi, dq, p, psi_coef, gcoef, xcoef, (bf16*)dgw, (bf16*)dxw, rows);
+  else
+    hipLaunchKernelGGL(gate_bwd3_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const float*)gw,
+                       (const float*)xw, gab, xab, wpsi, dq, p, psi_coef, gcoef, xcoef, (float*)dgw, (float*)dxw,
+                       rows);
+  return check_launch("gate_bwd3");
+}
+
+}  // extern "C"

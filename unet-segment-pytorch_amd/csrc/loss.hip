@@ -1,0 +1,217 @@
+// loss.hip — fused DiceBCE / Dice / BalancedCE loss and gradient (unet/utils/loss.py:18-191).
+//
+// Pass 1 (reduce): per image n and 256-pixel-range block, softmax + cross entropy per pixel and the
+//   sums  n0 = #[t=0], n1 = #[t=1], S0 = Σ_{t=0} ce, S1 = Σ_{t=1} ce, and per class c:
+//   I_c = Σ p_c [t=c], P_c = Σ p_c, T_c = #[t=c].           (loss.py:63-73 and 129-148)
+// Finalize (one block): loss scalar and per-(n, c) gradient coefficients, in fp64.
+// Pass 2 (grad): dz_k = gout · ( w_t (p_k − [k=t]) + G_k p_k [k∈D] − p_k Σ_{c∈D} G_c p_c ),
+//   G_c = gA_nc [t=c] + gB_nc,  w_t = BalancedCE per-pixel weight (labels 0/1 only, loss.py:136-145).
+// The per-image Python loop with boolean-mask indexing of the reference (loss.py:134-145) becomes
+// these device reductions: no host synchronisation.
+#include "common.h"
+
+namespace unet {
+
+constexpr int LMAXK = 16;
+
+static inline int loss_rows(long long HW) {
+  long long r = (HW + 4095) / 4096;
+  if (r > 256) r = 256;
+  if (r < 1) r = 1;
+  return (int)r;
+}
+
+template <int KT>
+__global__ void loss_reduce_kernel(long long N, int K_, long long HW, const float* z, const int64_t* t, float* part,
+                                   int rows) {
+  __shared__ float sh[8];
+  const int K = KT ? KT : K_;
+  const int F = 4 + 3 * K;
+  const long long n = blockIdx.y;
+  const long long per = (HW + rows - 1) / rows;
+  const long long q0 = blockIdx.x * per, q1 = min(HW, q0 + per);
+  float acc[4 + 3 * (KT ? KT : LMAXK)];
+#pragma unroll
+  for (int f = 0; f < 4 + 3 * (KT ? KT : LMAXK); ++f) acc[f] = 0.f;
+  for (long long q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+    const float* zp = z + n * K * HW + q;
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < (KT ? KT : LMAXK); ++k) if (k < K) m = fmaxf(m, zp[k * HW]);
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < (KT ? KT : LMAXK); ++k) if (k < K) se += __expf(zp[k * HW] - m);
+    const float lse = m + __logf(se);
+    int tv = (int)t[n * HW + q];
+    if (tv < 0 || tv >= K) tv = -1;  // out-of-range label (the reference raises): contributes nothing
+    const float ce = tv >= 0 ? lse - zp[tv * HW] : 0.f;
+    if (tv == 0) { acc[0] += 1.f; acc[2] += ce; }
+    if (tv == 1) { acc[1] += 1.f; acc[3] += ce; }
+    const float inv = 1.f / se;
+#pragma unroll
+    for (int k = 0; k < (KT ? KT : LMAXK); ++k) {
+      if (k >= K) break;
+      const float pk = __expf(zp[k * HW] - m) * inv;
+      acc[4 + 3 * k + 1] += pk;
+      if (tv == k) { acc[4 + 3 * k] += pk; acc[4 + 3 * k + 2] += 1.f; }
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < 4 + 3 * (KT ? KT : LMAXK); ++f) {
+    if (f >= F) break;
+    float v = wave_sum(acc[f]);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sh[w];
+      part[((size_t)n * rows + blockIdx.x) * F + f] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// one block, one thread per image; then thread 0 combines
+// coef layout [N][2 + 2K]: w0, w1, gA[K], gB[K]
+__global__ void loss_finalize_kernel(const float* part, int rows, long long N, int K, float ce_w, float dice_w,
+                                     float class_w, float ce_smooth, float dice_smooth, int ignore_bg, int reduction,
+                                     float* loss, float* coef) {
+  extern __shared__ double dsh[];  // [N] ce terms, [N*K] dice terms
+  const int F = 4 + 3 * K;
+  const int c_lo = (ignore_bg && K > 1) ? 1 : 0;
+  const int nd = K - c_lo;
+  const double wred = reduction == 0 ? 1.0 / ((double)N * nd) : 1.0;  // mean / sum / none(=1, gout per elem)
+  for (long long n = threadIdx.x; n < N; n += blockDim.x) {
+    double s[4 + 3 * LMAXK];
+    for (int f = 0; f < F; ++f) s[f] = 0;
+    for (int r = 0; r < rows; ++r)
+      for (int f = 0; f < F; ++f) s[f] += part[((size_t)n * rows + r) * F + f];
+    const double n0 = (double)(float)(s[0]) + ce_smooth, n1 = (double)(float)(s[1]) + ce_smooth;
+    const double w0 = (1.0 - class_w) / n0, w1 = class_w / n1;
+    dsh[n] = w0 * s[2] + w1 * s[3];
+    float* cf = coef + n * (2 + 2 * K);
+    cf[0] = (float)(ce_w * w0 / (double)N);
+    cf[1] = (float)(ce_w * w1 / (double)N);
+    for (int c = 0; c < K; ++c) {
+      const double I = s[4 + 3 * c], P = s[4 + 3 * c + 1], T = s[4 + 3 * c + 2];
+      const double U = P + T + dice_smooth;
+      const double D = (2.0 * I + dice_smooth) / U;
+      double gA = 0, gB = 0;
+      if (c >= c_lo) {
+        gA = -2.0 * dice_w * wred / U;
+        gB = dice_w * wred * (2.0 * I + dice_smooth) / (U * U);
+      }
+      cf[2 + c] = (float)gA;
+      cf[2 + K + c] = (float)gB;
+      dsh[N + n * K + c] = D;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (reduction == 2) {  // DiceLoss(reduction='none'): per-(n, c) 1 - D
+      for (long long n = 0; n < N; ++n)
+        for (int c = c_lo; c < K; ++c) loss[n * nd + (c - c_lo)] = (float)(1.0 - dsh[N + n * K + c]);
+      return;
+    }
+    double ce = 0, dsum = 0;
+    for (long long n = 0; n < N; ++n) {
+      ce += dsh[n];
+      for (int c = c_lo; c < K; ++c) dsum += dsh[N + n * K + c];
+    }
+    ce /= (double)N;
+    double dl = reduction == 0 ? 1.0 - dsum / ((double)N * nd) : (double)N * nd - dsum;
+    loss[0] = (float)(ce_w * ce + dice_w * dl);
+  }
+}
+
+template <int KT>
+__global__ void loss_grad_kernel(long long N, int K_, long long HW, const float* z, const int64_t* t, const float* coef,
+                                 const float* gout, int gout_per_elem, int c_lo, float* dz) {
+  constexpr int KM = KT ? KT : LMAXK;
+  const int K = KT ? KT : K_;
+  const long long total = N * HW;
+  const int nd = K - c_lo;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long n = e / HW, q = e % HW;
+    const float* zp = z + n * K * HW + q;
+    const float* cf = coef + n * (2 + 2 * K);
+    float p[KM];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) if (k < K) m = fmaxf(m, zp[k * HW]);
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) { p[k] = (k < K) ? __expf(zp[k * HW] - m) : 0.f; se += p[k]; }
+    const float inv = 1.f / se;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) p[k] *= inv;
+    int tv = (int)t[n * HW + q];
+    if (tv < 0 || tv >= K) tv = -1;
+    const float wt = tv == 0 ? cf[0] : (tv == 1 ? cf[1] : 0.f);
+    float G[KM];
+    float sgp = 0.f;
+#pragma unroll
+    for (int c = 0; c < KM; ++c) {
+      float g = 0.f;
+      if (c < K && c >= c_lo) {
+        g = (tv == c ? cf[2 + c] : 0.f) + cf[2 + K + c];
+        if (gout_per_elem) g *= gout[n * nd + c - c_lo];
+      }
+      G[c] = g;
+      sgp += g * p[c];
+    }
+    const float go = gout_per_elem ? 1.f : gout[0];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (k >= K) break;
+      const float ce = wt * (p[k] - (k == tv ? 1.f : 0.f));
+      dz[n * K * HW + k * HW + q] = go * (ce + G[k] * p[k] - p[k] * sgp);
+    }
+  }
+}
+
+}  // namespace unet
+
+using namespace unet;
+
+extern "C" {
+
+int unet_loss_rows(long long HW) { return loss_rows(HW); }
+
+int unet_loss_reduce(long long N, int K, long long HW, const float* z, const int64_t* t, float* partial, void* stream) {
+  if (K < 1 || K > LMAXK) { set_error("unet_loss_reduce: n_classes must be in [1, 16]"); return UNET_ERR_UNSUPPORTED; }
+  const int rows = loss_rows(HW);
+  if (K == 2)
+    hipLaunchKernelGGL(loss_reduce_kernel<2>, dim3(rows, N), dim3(256), 0, (hipStream_t)stream, N, K, HW, z, t, partial,
+                       rows);
+  else
+    hipLaunchKernelGGL(loss_reduce_kernel<0>, dim3(rows, N), dim3(256), 0, (hipStream_t)stream, N, K, HW, z, t, partial,
+                       rows);
+  return check_launch("loss_reduce");
+}
+
+int unet_loss_finalize(const float* partial, int rows, long long N, int K, float ce_w, float dice_w, float class_w,
+                       float ce_smooth, float dice_smooth, int ignore_bg, int reduction, float* loss, float* coef,
+                       void* stream) {
+  const size_t shm = (size_t)(N + N * K) * sizeof(double);
+  if (shm > 60000) { set_error("unet_loss_finalize: batch too large"); return UNET_ERR_UNSUPPORTED; }
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), shm, (hipStream_t)stream, partial, rows, N, K, ce_w,
+                     dice_w, class_w, ce_smooth, dice_smooth, ignore_bg, reduction, loss, coef);
+  return check_launch("loss_finalize");
+}
+
+int unet_loss_grad(long long N, int K, long long HW, const float* z, const int64_t* t, const float* coef,
+                   const float* gout, int gout_per_elem, int ignore_bg, float* dz, void* stream) {
+  long long b = (N * HW + 255) / 256;
+  if (b > 8192) b = 8192;
+  const int c_lo = (ignore_bg && K > 1) ? 1 : 0;
+  if (K == 2)
+    hipLaunchKernelGGL(loss_grad_kernel<2>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, N, K, HW, z, t, coef, gout,
+                       gout_per_elem, c_lo, dz);
+  else
+    hipLaunchKernelGGL(loss_grad_kernel<0>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, N, K, HW, z, t, coef, gout,
+                       gout_per_elem, c_lo, dz);
+  return check_launch("loss_grad");
+}
+
+}  // extern "C"

@@ -1,0 +1,397 @@
+// misc.hip — bilinear adjoint, NCHW resize (deep-supervision heads), OutConv, layout, fill.
+#include "src_gather.h"
+
+namespace unet {
+
+// sum over destination indices u in [0, up) whose interpolation touches source index i
+// (weight (1-l) on i0, l on i1 — PyTorch's linear rule, align_corners=True)
+__device__ __forceinline__ void up_range(float scale, int i, int in_size, int up, int& lo, int& hi) {
+  if (scale > 0.f) {
+    lo = (int)floorf((float)(i - 1) / scale) - 1;
+    hi = (int)ceilf((float)(i + 1) / scale) + 1;
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > up - 1 ? up - 1 : hi;
+  } else {
+    lo = 0;
+    hi = up - 1;
+  }
+}
+__device__ __forceinline__ float up_weight(float scale, int u, int in_size, int i) {
+  int i0, i1;
+  float l;
+  lin_idx(scale, u, in_size, i0, i1, l);
+  return (i0 == i ? 1.f - l : 0.f) + (i1 == i ? l : 0.f);
+}
+
+// NHWC gather adjoint: dx[n,i,j,c] (+)= Σ_{u,v} wy(u,i) wx(v,j) d_up[n, u+pt, v+pl, c]
+__global__ void upsample_bwd_kernel(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pt, int pl, int Hp,
+                                    int Wp, float sh, float sw, const float* dup, float* dx, int accum) {
+  const long long total = N * Hs * (long long)Ws * C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int c = e % C;
+    long long t = e / C;
+    const int j = t % Ws;
+    t /= Ws;
+    const int i = t % Hs;
+    const long long n = t / Hs;
+    int ulo, uhi, vlo, vhi;
+    up_range(sh, i, Hs, up_h, ulo, uhi);
+    up_range(sw, j, Ws, up_w, vlo, vhi);
+    float acc = 0.f;
+    for (int u = ulo; u <= uhi; ++u) {
+      const float wy = up_weight(sh, u, Hs, i);
+      if (wy == 0.f) continue;
+      const int yy = u + pt;
+      if (yy < 0 || yy >= Hp) continue;
+      float racc = 0.f;
+      for (int v = vlo; v <= vhi; ++v) {
+        const float wx = up_weight(sw, v, Ws, j);
+        if (wx == 0.f) continue;
+        const int xx = v + pl;
+        if (xx < 0 || xx >= Wp) continue;
+        racc += wx * dup[((n * Hp + yy) * (long long)Wp + xx) * C + c];
+      }
+      acc += wy * racc;
+    }
+    dx[e] = accum ? dx[e] + acc : acc;
+  }
+}
+
+// fp32 NCHW bilinear (align_corners=True) forward: y[nc, u, v]
+__global__ void resize_nchw_kernel(long long NC, int Hi, int Wi, int Ho, int Wo, float sh, float sw, const float* x,
+                                   float* y) {
+  const long long total = NC * Ho * (long long)Wo;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int v = e % Wo;
+    long long t = e / Wo;
+    const int u = t % Ho;
+    const long long nc = t / Ho;
+    int y0, y1, x0, x1;
+    float ly, lx;
+    lin_idx(sh, u, Hi, y0, y1, ly);
+    lin_idx(sw, v, Wi, x0, x1, lx);
+    const float* p = x + nc * Hi * (long long)Wi;
+    const float a = p[y0 * Wi + x0], b = p[y0 * Wi + x1], c = p[y1 * Wi + x0], d = p[y1 * Wi + x1];
+    y[e] = (1.f - ly) * ((1.f - lx) * a + lx * b) + ly * ((1.f - lx) * c + lx * d);
+  }
+}
+
+__global__ void resize_nchw_bwd_kernel(long long NC, int Hi, int Wi, int Ho, int Wo, float sh, float sw, const float* dy,
+                                       float* dx, int accum) {
+  const long long total = NC * Hi * (long long)Wi;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int j = e % Wi;
+    long long t = e / Wi;
+    const int i = t % Hi;
+    const long long nc = t / Hi;
+    int ulo, uhi, vlo, vhi;
+    up_range(sh, i, Hi, Ho, ulo, uhi);
+    up_range(sw, j, Wi, Wo, vlo, vhi);
+    const float* p = dy + nc * Ho * (long long)Wo;
+    float acc = 0.f;
+    for (int u = ulo; u <= uhi; ++u) {
+      const float wy = up_weight(sh, u, Hi, i);
+      if (wy == 0.f) continue;
+      float racc = 0.f;
+      for (int v = vlo; v <= vhi; ++v) {
+        const float wx = up_weight(sw, v, Wi, j);
+        if (wx != 0.f) racc += wx * p[u * (long long)Wo + v];
+      }
+      acc += wy * racc;
+    }
+    dx[e] = accum ? dx[e] + acc : acc;
+  }
+}
+
+// ---- OutConv: logits[n,k,h,w] = b[k] + Σ_c w[k][c] · act(y)[n,h,w,c]   (layers.py:120) ----------------
+constexpr int OC_MAXK = 8;
+
+template <typename T>
+__global__ void outconv_fwd_kernel(long long P, int HW, int C, int K, const T* y, const float* sc, const float* sf,
+                                   int relu, const float* w, const float* b, float* out) {
+  extern __shared__ float ws[];  // [K][C] then scale/shift
+  for (int i = threadIdx.x; i < K * C; i += blockDim.x) ws[i] = w[i];
+  float* s_sc = ws + K * C;
+  float* s_sf = s_sc + C;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    s_sc[i] = sc ? sc[i] : 1.f;
+    s_sf[i] = sf ? sf[i] : 0.f;
+  }
+  __syncthreads();
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < P; q += (long long)gridDim.x * blockDim.x) {
+    float acc[OC_MAXK];
+#pragma unroll
+    for (int k = 0; k < OC_MAXK; ++k) acc[k] = (k < K) ? b[k] : 0.f;
+    const T* yp = y + q * C;
+    for (int c = 0; c < C; ++c) {
+      float a = to_f(yp[c]) * s_sc[c] + s_sf[c];
+      if (relu) a = fmaxf(a, 0.f);
+#pragma unroll
+      for (int k = 0; k < OC_MAXK; ++k)
+        if (k < K) acc[k] += ws[k * C + c] * a;
+    }
+    const long long n = q / HW, hw = q % HW;
+#pragma unroll
+    for (int k = 0; k < OC_MAXK; ++k)
+      if (k < K) out[(n * K + k) * HW + hw] = acc[k];
+  }
+}
+
+// channel lanes x pixel rows: da[p][c] (+)= Σ_k w[k][c] dl[k][p]; partial dW[k][c], db[k]
+template <typename T>
+__global__ void outconv_bwd_kernel(long long P, int HW, int C, int CL, int K, const T* y, const float* sc,
+                                   const float* sf, int relu, const float* w, const float* dl, float* da, int accum,
+                                   float* part, int rows) {
+  __shared__ float sh[256];
+  const int tid = threadIdx.x;
+  const int cx = tid % CL, py = tid / CL, R = blockDim.x / CL;
+  const int c = blockIdx.x * CL + cx;
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.y * per, p1 = min(P, p0 + per);
+  float dw[OC_MAXK], db[OC_MAXK], wk[OC_MAXK];
+#pragma unroll
+  for (int k = 0; k < OC_MAXK; ++k) { dw[k] = 0.f; db[k] = 0.f; wk[k] = (k < K && c < C) ? w[k * C + c] : 0.f; }
+  const float s = (c < C && sc) ? sc[c] : 1.f, f = (c < C && sf) ? sf[c] : 0.f;
+  for (long long q = p0 + py; q < p1; q += R) {
+    const long long n = q / HW, hw = q % HW;
+    float g = 0.f;
+    float dlk[OC_MAXK];
+#pragma unroll
+    for (int k = 0; k < OC_MAXK; ++k) {
+      dlk[k] = (k < K) ? dl[(n * K + k) * HW + hw] : 0.f;
+      g += wk[k] * dlk[k];
+      db[k] += dlk[k];
+    }
+    if (c < C) {
+      float a = to_f(y[q * C + c]) * s + f;
+      if (relu) a = fmaxf(a, 0.f);
+#pragma unroll
+      for (int k = 0; k < OC_MAXK; ++k) dw[k] += dlk[k] * a;
+      float* o = da + q * C + c;
+      *o = accum ? *o + g : g;
+    }
+  }
+  // reduce over the R pixel rows sharing a channel lane
+  const int F = K + 1;
+  for (int k = 0; k < F; ++k) {
+    float v = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < OC_MAXK; ++kk) if (kk == k) v = dw[kk];
+    if (k == K) v = 0.f;
+    sh[tid] = v;
+    __syncthreads();
+    if (py == 0 && c < C && k < K) {
+      float a = 0.f;
+      for (int r = 0; r < R; ++r) a += sh[r * CL + cx];
+      part[((size_t)blockIdx.y * (K + 1) + k) * C + c] = a;
+    }
+    __syncthreads();
+  }
+  // db: only channel-block 0 writes it (every lane saw all pixels of its rows)
+  if (blockIdx.x == 0) {
+    for (int k = 0; k < K; ++k) {
+      float v = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < OC_MAXK; ++kk) if (kk == k) v = db[kk];
+      sh[tid] = (cx == 0) ? v : 0.f;
+      __syncthreads();
+      if (tid == 0) {
+        float a = 0.f;
+        for (int r = 0; r < R; ++r) a += sh[r * CL];
+        part[((size_t)blockIdx.y * (K + 1) + K) * C + k] = a;  // db stored in row K, column k
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void outconv_bwd_finalize_kernel(const float* part, int rows, int C, int K, float* dw, float* db, int accum) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = K * C + K;
+  if (e >= total) return;
+  double s = 0;
+  if (e < K * C) {
+    const int k = e / C, c = e % C;
+    for (int r = 0; r < rows; ++r) s += part[((size_t)r * (K + 1) + k) * C + c];
+    dw[e] = accum ? dw[e] + (float)s : (float)s;
+  } else {
+    const int k = e - K * C;
+    for (int r = 0; r < rows; ++r) s += part[((size_t)r * (K + 1) + K) * C + k];
+    db[k] = accum ? db[k] + (float)s : (float)s;
+  }
+}
+
+// ---- layout ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(long long N, int C, int H, int W, const float* x, T* y) {
+  const long long total = N * C * (long long)H * W;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int c = e % C;
+    const long long p = e / C;
+    const long long hw = p % ((long long)H * W), n = p / ((long long)H * W);
+    y[e] = from_f<T>(x[(n * C + c) * (long long)H * W + hw]);
+  }
+}
+template <typename T>
+__global__ void nhwc_to_nchw_kernel(long long N, int C, int H, int W, const T* x, const float* sc, const float* sf,
+                                    int relu, float* y) {
+  const long long total = N * C * (long long)H * W;
+  const long long HW = (long long)H * W;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long hw = e % HW;
+    const long long t = e / HW;
+    const int c = t % C;
+    const long long n = t / C;
+    float v = to_f(x[(n * HW + hw) * C + c]);
+    if (sc) v = v * sc[c] + sf[c];
+    if (relu) v = fmaxf(v, 0.f);
+    y[e] = v;
+  }
+}
+// x * sigmoid(psi) materialised as NCHW fp32 (standalone AttentionGate output, layers.py:192)
+template <typename T>
+__global__ void gated_to_nchw_kernel(long long N, int C, int H, int W, const T* x, const float* sc, const float* sf,
+                                     int relu, const float* p, const float* ab, float* y) {
+  const long long total = N * C * (long long)H * W;
+  const long long HW = (long long)H * W;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long hw = e % HW;
+    const long long t = e / HW;
+    const int c = t % C;
+    const long long n = t / C;
+    float v = to_f(x[(n * HW + hw) * C + c]) * sc[c] + sf[c];
+    if (relu) v = fmaxf(v, 0.f);
+    y[e] = v * sigmoidf_(p[n * HW + hw] * ab[0] + ab[1]);
+  }
+}
+__global__ void fill_kernel(float* x, long long n, float v) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) x[e] = v;
+}
+
+static inline int grid_for(long long total) {
+  long long b = (total + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+static inline int chan_lanes_m(int C) {
+  int cl = 1;
+  while (cl < C && cl < 64) cl <<= 1;
+  return cl;
+}
+static inline int oc_rows(long long P) {
+  long long r = (P + 1023) / 1024;
+  if (r > 1024) r = 1024;
+  if (r < 1) r = 1;
+  return (int)r;
+}
+
+}  // namespace unet
+
+using namespace unet;
+
+extern "C" {
+
+int unet_upsample_bwd(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pad_t, int pad_l, int Hp, int Wp,
+                      float sh, float sw, const float* d_up, float* dx, int accum, void* stream) {
+  const long long total = N * Hs * (long long)Ws * C;
+  hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, Hs, Ws,
+                     up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
+  return check_launch("upsample_bwd");
+}
+
+int unet_resize_nchw(long long NC, int Hi, int Wi, int Ho, int Wo, float sh, float sw, const float* x, float* y,
+                     void* stream) {
+  hipLaunchKernelGGL(resize_nchw_kernel, dim3(grid_for(NC * Ho * (long long)Wo)), dim3(256), 0, (hipStream_t)stream,
+                     NC, Hi, Wi, Ho, Wo, sh, sw, x, y);
+  return check_launch("resize_nchw");
+}
+
+int unet_resize_nchw_bwd(long long NC, int Hi, int Wi, int Ho, int Wo, float sh, float sw, const float* dy, float* dx,
+                         int accum, void* stream) {
+  hipLaunchKernelGGL(resize_nchw_bwd_kernel, dim3(grid_for(NC * Hi * (long long)Wi)), dim3(256), 0,
+                     (hipStream_t)stream, NC, Hi, Wi, Ho, Wo, sh, sw, dy, dx, accum);
+  return check_launch("resize_nchw_bwd");
+}
+
+int unet_outconv_rows(long long P) { return oc_rows(P); }
+
+int unet_outconv_fwd(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
+                     const float* shift, int relu, const float* w, const float* b, float* logits, void* stream) {
+  if (K > OC_MAXK || K < 1) { set_error("unet_outconv_fwd: n_classes > 8 unsupported"); return UNET_ERR_UNSUPPORTED; }
+  const long long P = N * H * (long long)W;
+  const size_t shm = (size_t)(K * C + 2 * C) * sizeof(float);
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(outconv_fwd_kernel<bf16>, dim3(grid_for(P)), dim3(256), shm, (hipStream_t)stream, P, H * W, C, K,
+                       (const bf16*)y, scale, shift, relu, w, b, logits);
+  else
+    hipLaunchKernelGGL(outconv_fwd_kernel<float>, dim3(grid_for(P)), dim3(256), shm, (hipStream_t)stream, P, H * W, C,
+                       K, (const float*)y, scale, shift, relu, w, b, logits);
+  return check_launch("outconv_fwd");
+}
+
+int unet_outconv_bwd(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
+                     const float* shift, int relu, const float* w, const float* dl, float* da, int accum, float* partial,
+                     void* stream) {
+  if (K > OC_MAXK || K < 1 || C < K) { set_error("unet_outconv_bwd: need 1 <= n_classes <= min(8, C)"); return UNET_ERR_UNSUPPORTED; }
+  const long long P = N * H * (long long)W;
+  const int cl = chan_lanes_m(C), rows = oc_rows(P);
+  dim3 grid(cdiv(C, cl), rows);
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(outconv_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, H * W, C, cl, K,
+                       (const bf16*)y, scale, shift, relu, w, dl, da, accum, partial, rows);
+  else
+    hipLaunchKernelGGL(outconv_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, P, H * W, C, cl, K,
+                       (const float*)y, scale, shift, relu, w, dl, da, accum, partial, rows);
+  return check_launch("outconv_bwd");
+}
+
+int unet_outconv_bwd_finalize(const float* partial, int rows, int C, int K, float* dw, float* db, int accum,
+                              void* stream) {
+  const int total = K * C + K;
+  hipLaunchKernelGGL(outconv_bwd_finalize_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, partial,
+                     rows, C, K, dw, db, accum);
+  return check_launch("outconv_bwd_finalize");
+}
+
+int unet_nchw_to_nhwc(int dtype, long long N, int C, int H, int W, const float* x, void* y, void* stream) {
+  const long long total = N * C * (long long)H * W;
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H, W,
+                       x, (bf16*)y);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H,
+                       W, x, (float*)y);
+  return check_launch("nchw_to_nhwc");
+}
+
+int unet_nhwc_to_nchw(int dtype, long long N, int C, int H, int W, const void* x, const float* scale,
+                      const float* shift, int relu, float* y, void* stream) {
+  const long long total = N * C * (long long)H * W;
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H, W,
+                       (const bf16*)x, scale, shift, relu, y);
+  else
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H,
+                       W, (const float*)x, scale, shift, relu, y);
+  return check_launch("nhwc_to_nchw");
+}
+
+int unet_gated_to_nchw(int dtype, long long N, int C, int H, int W, const void* x, const float* scale,
+                       const float* shift, int relu, const float* p, const float* psi_ab, float* y, void* stream) {
+  const long long total = N * C * (long long)H * W;
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(gated_to_nchw_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H,
+                       W, (const bf16*)x, scale, shift, relu, p, psi_ab, y);
+  else
+    hipLaunchKernelGGL(gated_to_nchw_kernel<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H,
+                       W, (const float*)x, scale, shift, relu, p, psi_ab, y);
+  return check_launch("gated_to_nchw");
+}
+
+int unet_fill_f32(float* x, long long n, float v, void* stream) {
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, v);
+  return check_launch("fill");
+}
+
+}  // extern "C"

@@ -1,0 +1,163 @@
+"""autograd.Function wrappers: the reference's modules as HIP launch plans.
+
+`run_network` serves UNet / AttentionUNet (whole-network plan with cross-module fusion);
+`run_module` serves a standalone DoubleConv / Down / Up / AttentionUp / AttentionGate / OutConv call
+(NCHW fp32 in and out, exactly like the reference module).  Param grads are returned through
+autograd, so `loss.backward()`, DDP hooks, clip_grad_norm_ and optimizers work unchanged.
+"""
+
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+from torch.autograd.function import once_differentiable
+
+from . import lib as L
+from .runtime import (Act, act_from_nchw, act_to_nchw, f32, get_precision, grad_nchw_to_nhwc, grad_nhwc_to_nchw,
+                      nchw_src, require_device, stream, up_scale, vp)
+from .stages import (DoubleConvStage, DownStage, GateStage, Grads, NetworkPlan, OutConvStage, UpStage)
+
+
+class _PlanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan, params: Sequence[torch.nn.Parameter], n_in: int, *tensors):
+        inputs = tensors[:n_in]
+        outs = plan.forward(list(inputs), [ctx.needs_input_grad[3 + i] for i in range(n_in)])
+        ctx.plan = plan
+        ctx.params = params
+        ctx.n_in = n_in
+        return tuple(outs)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, *gouts):
+        grads = Grads()
+        dins = ctx.plan.backward(list(gouts), grads)
+        pgrads = [grads.get(p) for p in ctx.params]
+        ctx.plan = None
+        return (None, None, None, *dins, *pgrads)
+
+
+def _apply(plan, module: torch.nn.Module, inputs: List[torch.Tensor]):
+    params = [p for p in module.parameters()]
+    track = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or any(i.requires_grad for i in inputs))
+    if not track:
+        return plan.forward(inputs, [False] * len(inputs))
+    return list(_PlanFn.apply(plan, params, len(inputs), *inputs, *params))
+
+
+# ------------------------------------------------------------------------------------------------
+class _NetPlan:
+    def __init__(self, model, attention: bool):
+        self.model = model
+        self.prec = get_precision(model)
+        self.training = model.training
+        self.net = NetworkPlan(model, attention)
+
+    def forward(self, inputs, needs):
+        x = inputs[0]
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.float().contiguous()
+        return self.net.forward(self.prec, x, self.training, needs[0])
+
+    def backward(self, gouts, grads):
+        return [self.net.backward(self.prec, gouts, grads)]
+
+
+def run_network(model, x: torch.Tensor, attention: bool):
+    require_device(x)
+    if x.dim() != 4 or x.shape[1] != model.n_channels:
+        raise RuntimeError(f"expected input of shape (N, {model.n_channels}, H, W), got {tuple(x.shape)}")
+    outs = _apply(_NetPlan(model, attention), model, [x])
+    return outs
+
+
+# ------------------------------------------------------------------------------------------------
+class _ModulePlan:
+    """Standalone module call: NCHW fp32 inputs -> NHWC operands -> stage -> NCHW fp32 output."""
+
+    def __init__(self, module, kind: str):
+        self.m = module
+        self.kind = kind
+        self.prec = get_precision(module)
+        self.training = module.training
+
+    def forward(self, inputs, needs):
+        prec, tr = self.prec, self.training
+        self.needs = needs
+        xs = [i if (i.dtype == torch.float32 and i.is_contiguous()) else i.float().contiguous() for i in inputs]
+        self.xs = xs
+        k = self.kind
+        if k == "double_conv":
+            x = xs[0]
+            N, C, H, W = x.shape
+            self.st = DoubleConvStage(self.m)
+            self.out = self.st.forward(prec, [nchw_src(x)], N, H, W, tr, keep=x)
+            return [act_to_nchw(self.out, prec)]
+        self.acts = [act_from_nchw(x, prec) for x in xs]
+        if k == "down":
+            self.st = DownStage(self.m)
+            self.out = self.st.forward(prec, self.acts[0], tr)
+            return [act_to_nchw(self.out, prec)]
+        if k in ("up", "attention_up"):
+            self.st = UpStage(self.m, k == "attention_up")
+            self.out = self.st.forward(prec, self.acts[0], self.acts[1], tr)
+            return [act_to_nchw(self.out, prec)]
+        if k == "out_conv":
+            self.st = OutConvStage(self.m)
+            return [self.st.forward(prec, self.acts[0])]
+        if k == "attention_gate":
+            g, x = self.acts
+            self.st = GateStage(self.m)
+            self.st.forward(prec, g, x, tr)
+            out = f32(x.N, x.C, x.H, x.W, device=x.data.device)
+            L.call("unet_gated_to_nchw", prec.code, x.N, x.C, x.H, x.W, vp(x.data), vp(x.ab[0]), vp(x.ab[1]),
+                   int(x.relu), vp(self.st.p), vp(self.st.psi_ab), vp(out), stream())
+            return [out]
+        raise ValueError(k)
+
+    def backward(self, gouts, grads):
+        prec = self.prec
+        g = gouts[0]
+        k = self.kind
+        if k == "double_conv":
+            x = self.xs[0]
+            self.out.grad = grad_nchw_to_nhwc(g)
+            self.out._grad_init = True
+            if self.needs[0]:
+                N, C, H, W = x.shape
+                gx = f32(N, H, W, C, device=x.device)
+                self.st.backward(prec, grads, {"mode": "f32", "out": gx, "accum": 0})
+                return [grad_nhwc_to_nchw(gx)]
+            self.st.backward(prec, grads, None)
+            return [None]
+        if k == "out_conv":
+            self.st.backward(prec, g, grads)
+        elif k == "attention_gate":
+            gact, xact = self.acts
+            d_xs = grad_nchw_to_nhwc(g)
+            d_gup = f32(xact.N, xact.H, xact.W, gact.C, device=g.device)
+            self.st.backward(prec, d_xs, grads, d_gup, 0)
+            gg, acc = gact.grad_target()
+            L.call("unet_upsample_bwd", gact.N, gact.C, gact.H, gact.W, xact.H, xact.W, 0, 0, xact.H, xact.W,
+                   up_scale(gact.H, xact.H), up_scale(gact.W, xact.W), vp(d_gup), vp(gg), acc, stream())
+        else:
+            self.out.grad = grad_nchw_to_nhwc(g)
+            self.out._grad_init = True
+            self.st.backward(prec, grads)
+        res = []
+        for a, need in zip(self.acts, self.needs):
+            if need and a.has_grad():
+                res.append(grad_nhwc_to_nchw(a.grad))
+            elif need:
+                res.append(torch.zeros(a.N, a.C, a.H, a.W, device=a.data.device))
+            else:
+                res.append(None)
+        return res
+
+
+def run_module(module, kind: str, *inputs: torch.Tensor) -> torch.Tensor:
+    for i in inputs:
+        require_device(i)
+    return _apply(_ModulePlan(module, kind), module, list(inputs))[0]

@@ -1,0 +1,135 @@
+"""ctypes binding of the C-ABI in include/unet_hip.h (libunet_hip.so, built for gfx950).
+
+This is the ONLY way the package reaches the device: there is no CPU fallback.  If the library is
+missing or no ROCm GPU is visible, every compute entry point raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (import first: libamdhip64.so.7 must resolve to the runtime torch loaded)
+
+_LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).resolve().parent / "libunet_hip.so"))
+
+F32, BF16 = 0, 1
+SRC_PLAIN, SRC_ACT, SRC_POOL_ACT, SRC_UP_ACT, SRC_NCHW_F32, SRC_UP_PLAIN = range(6)
+OUT_Y, OUT_F32, OUT_POOL_BWD = range(3)
+
+c_int, c_ll, c_float, c_vp, c_size = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+
+
+class Src(ctypes.Structure):
+    _fields_ = [("kind", c_int), ("C", c_int), ("H", c_int), ("W", c_int), ("data", c_vp), ("scale", c_vp),
+                ("shift", c_vp), ("relu", c_int), ("up_h", c_int), ("up_w", c_int), ("pad_t", c_int),
+                ("pad_l", c_int), ("sh", c_float), ("sw", c_float), ("gate_p", c_vp), ("gate_ab", c_vp)]
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("N", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
+                ("ksize", c_int), ("nsrc", c_int), ("src", Src * 2), ("weight", c_vp), ("out_mode", c_int),
+                ("out", c_vp), ("out2", c_vp), ("split", c_int), ("accum", c_int), ("accum2", c_int),
+                ("stats", c_vp), ("pool_src", Src)]
+
+
+class WgradDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("N", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
+                ("ksize", c_int), ("nsrc", c_int), ("src", Src * 2), ("dy", c_vp), ("dw", c_vp), ("accum", c_int),
+                ("workspace", c_vp)]
+
+
+# name -> (restype, argtypes); mirrors include/unet_hip.h
+_SIGS = {
+    "unet_last_error": (ctypes.c_char_p, []),
+    "unet_version": (c_int, []),
+    "unet_conv_mtiles": (c_int, [c_int, c_int, c_int]),
+    "unet_pack_weight": (c_int, [c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "unet_packed_weight_elems": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "unet_conv": (c_int, [ctypes.POINTER(ConvDesc), c_vp]),
+    "unet_wgrad_workspace": (c_size, [ctypes.POINTER(WgradDesc)]),
+    "unet_conv_wgrad": (c_int, [ctypes.POINTER(WgradDesc), c_vp]),
+    "unet_bn_finalize": (c_int, [c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_vp, c_vp,
+                                 c_vp, c_vp, c_vp]),
+    "unet_bn_eval_affine": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_vp]),
+    "unet_bn_bwd_reduce_rows": (c_int, [c_ll, c_int]),
+    "unet_bn_bwd_reduce": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "unet_bn_bwd_finalize": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "unet_bn_bwd_apply": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "unet_colsum": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp]),
+    "unet_gate_psi_rows": (c_int, [c_ll]),
+    "unet_gate_psi": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "unet_gate_bwd1": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                               c_vp, c_vp, c_vp]),
+    "unet_gate_bwd2_rows": (c_int, [c_ll, c_int]),
+    "unet_gate_bwd2": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_vp, c_vp, c_vp]),
+    "unet_gate_bwd3": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_vp, c_vp]),
+    "unet_upsample_bwd": (c_int, [c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
+                                  c_vp, c_vp, c_int, c_vp]),
+    "unet_resize_nchw": (c_int, [c_ll, c_int, c_int, c_int, c_int, c_float, c_float, c_vp, c_vp, c_vp]),
+    "unet_resize_nchw_bwd": (c_int, [c_ll, c_int, c_int, c_int, c_int, c_float, c_float, c_vp, c_vp, c_int, c_vp]),
+    "unet_outconv_rows": (c_int, [c_ll]),
+    "unet_outconv_fwd": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
+                                 c_vp]),
+    "unet_outconv_bwd": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
+                                 c_int, c_vp, c_vp]),
+    "unet_outconv_bwd_finalize": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "unet_nchw_to_nhwc": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "unet_nhwc_to_nchw": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "unet_gated_to_nchw": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "unet_fill_f32": (c_int, [c_vp, c_ll, c_float, c_vp]),
+    "unet_loss_rows": (c_int, [c_ll]),
+    "unet_loss_reduce": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp]),
+    "unet_loss_finalize": (c_int, [c_vp, c_int, c_ll, c_int, c_float, c_float, c_float, c_float, c_float, c_int, c_int,
+                                   c_vp, c_vp, c_vp]),
+    "unet_loss_grad": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
+}
+
+_lib = None
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def library_path() -> Path:
+    return _LIB_PATH
+
+
+def load(require_gpu: bool = False):
+    """Load (once) and return the ctypes library.  Raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise HipLibraryError(
+                f"unet HIP library not found at {_LIB_PATH}; build it with "
+                f"`make -C unet-segment-pytorch_amd/csrc` (or __graft_entry__.build()). There is no CPU fallback.")
+        lib = ctypes.CDLL(str(_LIB_PATH))
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    if require_gpu and not torch.cuda.is_available():
+        raise HipLibraryError("unet HIP path needs a ROCm GPU (MI355X / gfx950); none is visible.")
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.unet_last_error().decode() if _lib is not None else ""
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    check(rc, name)
+    return rc

@@ -1,0 +1,230 @@
+"""Runtime helpers for the HIP path: precision, streams, virtual activations, source descriptors."""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import lib as L
+
+# ------------------------------------------------------------------------------------------------
+# precision
+# ------------------------------------------------------------------------------------------------
+
+
+@dataclass(frozen=True)
+class Precision:
+    name: str
+    code: int
+    torch_dtype: torch.dtype
+
+
+FP32 = Precision("fp32", L.F32, torch.float32)
+BF16 = Precision("bf16", L.BF16, torch.bfloat16)
+_PRECISIONS = {"fp32": FP32, "float32": FP32, "bf16": BF16, "bfloat16": BF16}
+_default = _PRECISIONS[os.environ.get("UNET_PRECISION", "fp32").lower()]
+
+
+def set_precision(name: str) -> None:
+    """Default operand precision of the HIP kernels ('fp32' = reference numerics, 'bf16')."""
+    global _default
+    _default = _PRECISIONS[name.lower()]
+
+
+def get_precision(module: Optional[torch.nn.Module] = None) -> Precision:
+    if module is not None:
+        p = getattr(module, "hip_precision", None)
+        if p is not None:
+            return _PRECISIONS[p.lower()] if isinstance(p, str) else p
+    return _default
+
+
+# ------------------------------------------------------------------------------------------------
+# device plumbing
+# ------------------------------------------------------------------------------------------------
+
+def require_device(t: torch.Tensor, what: str = "input") -> None:
+    if not t.is_cuda:
+        raise RuntimeError(
+            f"unet HIP path: {what} is on {t.device}; this implementation runs only on a ROCm GPU "
+            f"(MI355X). Move the model and inputs to 'cuda'. The CPU restatement in oracle/ is test "
+            f"infrastructure, not a fallback.")
+    L.load(require_gpu=True)
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def vp(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def f32(*shape, device) -> torch.Tensor:
+    return torch.empty(*shape, dtype=torch.float32, device=device)
+
+
+def up_scale(in_size: int, out_size: int) -> float:
+    """fp32 align_corners scale exactly as ATen's area_pixel_compute_scale."""
+    if out_size <= 1:
+        return 0.0
+    return float(np.float32(in_size - 1) / np.float32(out_size - 1))
+
+
+def pack_weight(w: torch.Tensor, prec: Precision, transpose: bool) -> torch.Tensor:
+    cout, cin, k = w.shape[0], w.shape[1], w.shape[2]
+    n = L.load().unet_packed_weight_elems(prec.code, cout, cin, k, int(transpose))
+    out = torch.empty(n, dtype=prec.torch_dtype, device=w.device)
+    wc = w.detach()
+    if wc.dtype != torch.float32 or not wc.is_contiguous():
+        wc = wc.float().contiguous()
+    L.call("unet_pack_weight", prec.code, vp(wc), vp(out), cout, cin, k, int(transpose), stream())
+    return out
+
+
+def fill_zero(t: torch.Tensor) -> None:
+    L.call("unet_fill_f32", vp(t), t.numel(), 0.0, stream())
+
+
+# ------------------------------------------------------------------------------------------------
+# virtual activations
+# ------------------------------------------------------------------------------------------------
+
+
+class Act:
+    """A stored NHWC tensor plus the per-channel affine (+ReLU) that makes it the reference's
+    activation (relu(bn(y)) of a DoubleConv half, or the identity for a materialised input).
+    `grad` is the fp32 NHWC gradient w.r.t. that activation, accumulated by its consumers."""
+
+    __slots__ = ("data", "N", "H", "W", "C", "ab", "relu", "mean", "invstd", "grad", "_grad_init", "keep")
+
+    def __init__(self, data: torch.Tensor, ab: Optional[torch.Tensor], relu: bool,
+                 mean: Optional[torch.Tensor] = None, invstd: Optional[torch.Tensor] = None):
+        self.data = data
+        self.N, self.H, self.W, self.C = data.shape
+        self.ab = ab          # fp32 [2, C] (scale; shift) or None
+        self.relu = relu
+        self.mean = mean
+        self.invstd = invstd
+        self.grad = None
+        self._grad_init = False
+        self.keep = None
+
+    @property
+    def scale(self):
+        return self.ab[0]
+
+    @property
+    def shift(self):
+        return self.ab[1]
+
+    @property
+    def pixels(self) -> int:
+        return self.N * self.H * self.W
+
+    # -- gradient buffer management --
+    def grad_target(self):
+        """(buffer, accumulate) for the next contribution to this activation's gradient."""
+        if self.grad is None:
+            self.grad = f32(self.N, self.H, self.W, self.C, device=self.data.device)
+        acc = self._grad_init
+        self._grad_init = True
+        return self.grad, int(acc)
+
+    def grad_zeroed(self) -> torch.Tensor:
+        if self.grad is None:
+            self.grad = f32(self.N, self.H, self.W, self.C, device=self.data.device)
+        if not self._grad_init:
+            fill_zero(self.grad)
+            self._grad_init = True
+        return self.grad
+
+    def has_grad(self) -> bool:
+        return self._grad_init
+
+    # -- source descriptors --
+    def _base(self, kind: int) -> L.Src:
+        s = L.Src()
+        s.kind = kind
+        s.C, s.H, s.W = self.C, self.H, self.W
+        s.data = self.data.data_ptr()
+        if self.ab is not None:
+            s.scale = self.ab[0].data_ptr()
+            s.shift = self.ab[1].data_ptr()
+        s.relu = int(self.relu)
+        return s
+
+    def src(self) -> L.Src:
+        return self._base(L.SRC_ACT if self.ab is not None else L.SRC_PLAIN)
+
+    def src_pool(self) -> L.Src:
+        assert self.ab is not None
+        return self._base(L.SRC_POOL_ACT)
+
+    def src_up(self, up_h: int, up_w: int, pad_t: int = 0, pad_l: int = 0) -> L.Src:
+        assert self.ab is not None
+        s = self._base(L.SRC_UP_ACT)
+        s.up_h, s.up_w, s.pad_t, s.pad_l = up_h, up_w, pad_t, pad_l
+        s.sh = up_scale(self.H, up_h)
+        s.sw = up_scale(self.W, up_w)
+        return s
+
+    def src_gated(self, p: torch.Tensor, psi_ab: torch.Tensor) -> L.Src:
+        s = self._base(L.SRC_ACT)
+        s.gate_p = p.data_ptr()
+        s.gate_ab = psi_ab.data_ptr()
+        return s
+
+
+def identity_ab(C: int, device) -> torch.Tensor:
+    ab = torch.empty(2, C, dtype=torch.float32, device=device)
+    L.call("unet_fill_f32", vp(ab[0]), C, 1.0, stream())
+    L.call("unet_fill_f32", vp(ab[1]), C, 0.0, stream())
+    return ab
+
+
+def act_from_nchw(x: torch.Tensor, prec: Precision) -> Act:
+    """Materialise an NCHW fp32 module input as an NHWC operand tensor (identity activation)."""
+    N, C, H, W = x.shape
+    xc = x.detach()
+    if xc.dtype != torch.float32 or not xc.is_contiguous():
+        xc = xc.float().contiguous()
+    y = torch.empty(N, H, W, C, dtype=prec.torch_dtype, device=x.device)
+    L.call("unet_nchw_to_nhwc", prec.code, N, C, H, W, vp(xc), vp(y), stream())
+    return Act(y, identity_ab(C, x.device), False)
+
+
+def nchw_src(x: torch.Tensor) -> L.Src:
+    s = L.Src()
+    s.kind = L.SRC_NCHW_F32
+    s.C, s.H, s.W = x.shape[1], x.shape[2], x.shape[3]
+    s.data = x.data_ptr()
+    return s
+
+
+def act_to_nchw(a: Act, prec: Precision) -> torch.Tensor:
+    out = torch.empty(a.N, a.C, a.H, a.W, dtype=torch.float32, device=a.data.device)
+    sc = vp(a.ab[0]) if a.ab is not None else None
+    sf = vp(a.ab[1]) if a.ab is not None else None
+    L.call("unet_nhwc_to_nchw", prec.code, a.N, a.C, a.H, a.W, vp(a.data), sc, sf, int(a.relu), vp(out), stream())
+    return out
+
+
+def grad_nchw_to_nhwc(g: torch.Tensor) -> torch.Tensor:
+    N, C, H, W = g.shape
+    gc = g.float().contiguous()
+    out = f32(N, H, W, C, device=g.device)
+    L.call("unet_nchw_to_nhwc", L.F32, N, C, H, W, vp(gc), vp(out), stream())
+    return out
+
+
+def grad_nhwc_to_nchw(g: torch.Tensor) -> torch.Tensor:
+    N, H, W, C = g.shape
+    out = f32(N, C, H, W, device=g.device)
+    L.call("unet_nhwc_to_nchw", L.F32, N, C, H, W, vp(g), None, None, 0, vp(out), stream())
+    return out

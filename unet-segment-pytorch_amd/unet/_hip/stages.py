@@ -1,0 +1,468 @@
+"""Stage executor: the reference's modules re-expressed as HIP launches on virtual activations.
+
+Each stage mirrors one reference module (file:line in the docstrings) and owns the kernel launches
+for its forward and backward.  Inter-module transforms (BN-apply + ReLU of the previous
+DoubleConv, MaxPool2d, bilinear up, pad, concat, attention multiply) are not launched at all: they
+are folded into the consuming conv's tile loader through `unet_src` descriptors.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from . import lib as L
+from .runtime import Act, Precision, f32, pack_weight, stream, up_scale, vp
+
+
+def _conv_desc(prec: Precision, N: int, H: int, W: int, cin: int, cout: int, k: int, srcs: List[L.Src],
+               weight: torch.Tensor) -> L.ConvDesc:
+    d = L.ConvDesc()
+    d.dtype = prec.code
+    d.N, d.H, d.W, d.Cin, d.Cout, d.ksize = N, H, W, cin, cout, k
+    d.nsrc = len(srcs)
+    for i, s in enumerate(srcs):
+        d.src[i] = s
+    d.weight = weight.data_ptr()
+    return d
+
+
+def _plain_src(t: torch.Tensor) -> L.Src:
+    s = L.Src()
+    s.kind = L.SRC_PLAIN
+    s.H, s.W, s.C = t.shape[1], t.shape[2], t.shape[3]
+    s.data = t.data_ptr()
+    return s
+
+
+class Grads(dict):
+    """param -> fp32 gradient tensor (assigned once per backward; accumulated if reused)."""
+
+    def put(self, p: torch.nn.Parameter, g: torch.Tensor):
+        if p in self:
+            self[p] = self[p] + g
+        else:
+            self[p] = g
+
+
+# ------------------------------------------------------------------------------------------------
+class ConvBN:
+    """nn.Conv2d(k, bias=False) -> nn.BatchNorm2d (-> ReLU): one half of DoubleConv
+    (layers.py:32-34 / 35-37) or a gate projection W_g / W_x (layers.py:151-160, relu=False)."""
+
+    def __init__(self, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, relu: bool):
+        self.conv, self.bn, self.relu = conv, bn, relu
+        self.k = conv.kernel_size[0]
+        self.cin, self.cout = conv.in_channels, conv.out_channels
+
+    # ---- forward ----
+    def forward(self, prec: Precision, srcs: List[L.Src], N: int, H: int, W: int, training: bool,
+                keep=None) -> Act:
+        dev = self.conv.weight.device
+        wp = pack_weight(self.conv.weight, prec, transpose=False)
+        y = torch.empty(N, H, W, self.cout, dtype=prec.torch_dtype, device=dev)
+        d = _conv_desc(prec, N, H, W, self.cin, self.cout, self.k, srcs, wp)
+        d.out_mode = L.OUT_Y
+        d.out = y.data_ptr()
+        bn = self.bn
+        ab = f32(2, self.cout, device=dev)
+        use_batch = training or not bn.track_running_stats
+        if use_batch:
+            mt = L.load().unet_conv_mtiles(N, H, W)
+            stats = f32(2, mt, self.cout, device=dev)
+            d.stats = stats.data_ptr()
+        L.call("unet_conv", d, stream())
+        mean = invstd = None
+        if use_batch:
+            mean = f32(self.cout, device=dev)
+            invstd = f32(self.cout, device=dev)
+            upd = training and bn.track_running_stats
+            mom = -1.0 if bn.momentum is None else float(bn.momentum)
+            L.call("unet_bn_finalize", vp(stats), mt, self.cout, N * H * W, vp(bn.weight), vp(bn.bias),
+                   vp(bn.running_mean) if upd else None, vp(bn.running_var) if upd else None,
+                   vp(bn.num_batches_tracked) if upd else None, mom, float(bn.eps), vp(mean), vp(invstd),
+                   vp(ab[0]), vp(ab[1]), stream())
+        else:
+            L.call("unet_bn_eval_affine", self.cout, vp(bn.weight), vp(bn.bias), vp(bn.running_mean),
+                   vp(bn.running_var), float(bn.eps), vp(ab[0]), vp(ab[1]), stream())
+        a = Act(y, ab, self.relu, mean, invstd)
+        a.keep = keep  # keeps the source tensors alive until backward
+        return a
+
+    # ---- backward ----
+    def bn_backward(self, prec: Precision, a: Act, grads: Grads) -> torch.Tensor:
+        """BatchNorm2d(+ReLU) backward: returns dy (op dtype, NHWC) at the conv output."""
+        dev = a.data.device
+        P, C = a.pixels, a.C
+        assert a.has_grad(), "activation gradient missing"
+        rows = L.load().unet_bn_bwd_reduce_rows(P, C)
+        part = f32(2, rows, C, device=dev)
+        L.call("unet_bn_bwd_reduce", prec.code, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+               int(a.relu), vp(a.mean), vp(a.invstd), vp(part), stream())
+        dgamma, dbeta, coef = f32(C, device=dev), f32(C, device=dev), f32(3, C, device=dev)
+        L.call("unet_bn_bwd_finalize", vp(part[0]), vp(part[1]), rows, C, P, vp(self.bn.weight), vp(a.mean),
+               vp(a.invstd), vp(dgamma), vp(dbeta), 0, vp(coef), stream())
+        grads.put(self.bn.weight, dgamma)
+        grads.put(self.bn.bias, dbeta)
+        dy = torch.empty(a.N, a.H, a.W, C, dtype=prec.torch_dtype, device=dev)
+        L.call("unet_bn_bwd_apply", prec.code, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+               int(a.relu), vp(coef), vp(dy), stream())
+        return dy
+
+    def conv_backward(self, prec: Precision, dy: torch.Tensor, srcs: List[L.Src], grads: Grads,
+                      dgrad: Optional[dict]):
+        """wgrad into grads[conv.weight]; dgrad routed by `dgrad`:
+        {'mode': 'f32', 'out': t, 'accum': 0/1, 'out2': t2, 'accum2': 0/1, 'split': s}
+        {'mode': 'pool', 'out': t (initialised), 'pool_src': Src}"""
+        N, H, W, cout = dy.shape
+        dev = dy.device
+        wd = L.WgradDesc()
+        wd.dtype = prec.code
+        wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize = N, H, W, self.cin, self.cout, self.k
+        wd.nsrc = len(srcs)
+        for i, s in enumerate(srcs):
+            wd.src[i] = s
+        wd.dy = dy.data_ptr()
+        dw = f32(self.cout, self.cin, self.k, self.k, device=dev)
+        wd.dw = dw.data_ptr()
+        wd.accum = 0
+        ws_bytes = L.load().unet_wgrad_workspace(wd)
+        ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+        wd.workspace = ws.data_ptr()
+        L.call("unet_conv_wgrad", wd, stream())
+        grads.put(self.conv.weight, dw)
+        if dgrad is None:
+            return
+        wt = pack_weight(self.conv.weight, prec, transpose=True)
+        d = _conv_desc(prec, N, H, W, self.cout, self.cin, self.k, [_plain_src(dy)], wt)
+        if dgrad["mode"] == "pool":
+            d.out_mode = L.OUT_POOL_BWD
+            d.out = dgrad["out"].data_ptr()
+            d.pool_src = dgrad["pool_src"]
+        else:
+            d.out_mode = L.OUT_F32
+            d.out = dgrad["out"].data_ptr()
+            d.accum = int(dgrad.get("accum", 0))
+            d.split = int(dgrad.get("split", self.cin))
+            o2 = dgrad.get("out2")
+            d.out2 = o2.data_ptr() if o2 is not None else None
+            d.accum2 = int(dgrad.get("accum2", 0))
+        L.call("unet_conv", d, stream())
+
+
+# ------------------------------------------------------------------------------------------------
+class DoubleConvStage:
+    """DoubleConv: (conv3x3 -> BN -> ReLU) x 2 — layers.py:16-41."""
+
+    def __init__(self, m):
+        seq = m.double_conv
+        self.c1 = ConvBN(seq[0], seq[1], True)
+        self.c2 = ConvBN(seq[3], seq[4], True)
+
+    def forward(self, prec, srcs, N, H, W, training, keep=None) -> Act:
+        self.srcs = srcs
+        self.a1 = self.c1.forward(prec, srcs, N, H, W, training, keep)
+        self.a2 = self.c2.forward(prec, [self.a1.src()], N, H, W, training)
+        return self.a2
+
+    def backward(self, prec, grads: Grads, dgrad: Optional[dict]):
+        dy2 = self.c2.bn_backward(prec, self.a2, grads)
+        g1, acc = self.a1.grad_target()
+        self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, {"mode": "f32", "out": g1, "accum": acc})
+        del dy2
+        dy1 = self.c1.bn_backward(prec, self.a1, grads)
+        self.c1.conv_backward(prec, dy1, self.srcs, grads, dgrad)
+
+
+# ------------------------------------------------------------------------------------------------
+class GateStage:
+    """AttentionGate — layers.py:126-192: W_g(g_up), W_x(x) (1x1 conv + BN), relu(sum), psi
+    (1x1 conv -> BN(1) -> sigmoid), x * psi.  g_up = bilinear(g, size=x) (:183)."""
+
+    def __init__(self, m):
+        self.cg = ConvBN(m.W_g[0], m.W_g[1], False)
+        self.cx = ConvBN(m.W_x[0], m.W_x[1], False)
+        self.psi_conv, self.psi_bn = m.psi[0], m.psi[1]
+        self.ci = self.cg.cout
+
+    def forward(self, prec, g: Act, x: Act, training: bool):
+        N, H, W = x.N, x.H, x.W
+        dev = x.data.device
+        self.g, self.x = g, x
+        self.src_g = g.src_up(H, W, 0, 0)
+        self.gw = self.cg.forward(prec, [self.src_g], N, H, W, training)
+        self.gw_src = [self.src_g]
+        self.xw = self.cx.forward(prec, [x.src()], N, H, W, training)
+        P = N * H * W
+        self.p = f32(N, H, W, device=dev)
+        rows = L.load().unet_gate_psi_rows(P)
+        part = f32(2, rows, device=dev)
+        self.wpsi = self.psi_conv.weight.detach().reshape(-1).float().contiguous()
+        L.call("unet_gate_psi", prec.code, P, self.ci, vp(self.gw.data), vp(self.xw.data), vp(self.gw.ab),
+               vp(self.xw.ab), vp(self.wpsi), vp(self.p), vp(part), stream())
+        bn = self.psi_bn
+        self.psi_ab = f32(2, 1, device=dev)
+        use_batch = training or not bn.track_running_stats
+        if use_batch:
+            self.psi_mean, self.psi_invstd = f32(1, device=dev), f32(1, device=dev)
+            upd = training and bn.track_running_stats
+            mom = -1.0 if bn.momentum is None else float(bn.momentum)
+            L.call("unet_bn_finalize", vp(part), rows, 1, P, vp(bn.weight), vp(bn.bias),
+                   vp(bn.running_mean) if upd else None, vp(bn.running_var) if upd else None,
+                   vp(bn.num_batches_tracked) if upd else None, mom, float(bn.eps), vp(self.psi_mean),
+                   vp(self.psi_invstd), vp(self.psi_ab[0]), vp(self.psi_ab[1]), stream())
+        else:
+            L.call("unet_bn_eval_affine", 1, vp(bn.weight), vp(bn.bias), vp(bn.running_mean), vp(bn.running_var),
+                   float(bn.eps), vp(self.psi_ab[0]), vp(self.psi_ab[1]), stream())
+
+    def gated_src(self) -> L.Src:
+        return self.x.src_gated(self.p, self.psi_ab)
+
+    def backward(self, prec, d_xs: torch.Tensor, grads: Grads, d_gup: torch.Tensor, d_gup_accum: int):
+        """d_xs: fp32 NHWC grad of x*s.  Adds into x.grad; writes/adds W_g's input-grad into d_gup
+        (fp32 NHWC at x's size, the upsampled-g space)."""
+        x = self.x
+        dev = x.data.device
+        P, Cx, Ci = x.pixels, x.C, self.ci
+        # (1) through x*s and the sigmoid; psi-BN backward sums
+        dx, dx_acc = x.grad_target()
+        dq = f32(P, device=dev)
+        rows1 = L.load().unet_gate_psi_rows(P)
+        part1 = f32(2, rows1, device=dev)
+        L.call("unet_gate_bwd1", prec.code, P, Cx, vp(d_xs), vp(x.data), vp(x.ab[0]), vp(x.ab[1]), int(x.relu), vp(self.p),
+               vp(self.psi_ab), vp(self.psi_mean), vp(self.psi_invstd), vp(dx), dx_acc, vp(dq), vp(part1), stream())
+        dgp, dbp, pcoef = f32(1, device=dev), f32(1, device=dev), f32(3, device=dev)
+        L.call("unet_bn_bwd_finalize", vp(part1[0]), vp(part1[1]), rows1, 1, P, vp(self.psi_bn.weight),
+               vp(self.psi_mean), vp(self.psi_invstd), vp(dgp), vp(dbp), 0, vp(pcoef), stream())
+        grads.put(self.psi_bn.weight, dgp)
+        grads.put(self.psi_bn.bias, dbp)
+        # (2) psi conv / relu / both BN backward sums
+        rows2 = L.load().unet_gate_bwd2_rows(P, Ci)
+        part2 = f32(4, rows2, Ci, device=dev)
+        L.call("unet_gate_bwd2", prec.code, P, Ci, vp(self.gw.data), vp(self.xw.data), vp(self.gw.ab),
+               vp(self.xw.ab), vp(self.gw.mean), vp(self.gw.invstd), vp(self.xw.mean), vp(self.xw.invstd),
+               vp(self.wpsi), vp(dq), vp(self.p), vp(pcoef), vp(part2), stream())
+        dgg, dbg, gcoef = f32(Ci, device=dev), f32(Ci, device=dev), f32(3, Ci, device=dev)
+        dgx, dbx, xcoef = f32(Ci, device=dev), f32(Ci, device=dev), f32(3, Ci, device=dev)
+        L.call("unet_bn_bwd_finalize", vp(part2[0]), vp(part2[1]), rows2, Ci, P, vp(self.cg.bn.weight),
+               vp(self.gw.mean), vp(self.gw.invstd), vp(dgg), vp(dbg), 0, vp(gcoef), stream())
+        L.call("unet_bn_bwd_finalize", vp(part2[0]), vp(part2[2]), rows2, Ci, P, vp(self.cx.bn.weight),
+               vp(self.xw.mean), vp(self.xw.invstd), vp(dgx), vp(dbx), 0, vp(xcoef), stream())
+        grads.put(self.cg.bn.weight, dgg)
+        grads.put(self.cg.bn.bias, dbg)
+        grads.put(self.cx.bn.weight, dgx)
+        grads.put(self.cx.bn.bias, dbx)
+        dwpsi = f32(Ci, device=dev)
+        L.call("unet_colsum", vp(part2[3]), rows2, Ci, vp(dwpsi), 0, stream())
+        grads.put(self.psi_conv.weight, dwpsi.view(1, Ci, 1, 1))
+        # (3) dgw, dxw
+        dgw = torch.empty(x.N, x.H, x.W, Ci, dtype=prec.torch_dtype, device=dev)
+        dxw = torch.empty_like(dgw)
+        L.call("unet_gate_bwd3", prec.code, P, Ci, vp(self.gw.data), vp(self.xw.data), vp(self.gw.ab),
+               vp(self.xw.ab), vp(self.wpsi), vp(dq), vp(self.p), vp(pcoef), vp(gcoef), vp(xcoef), vp(dgw), vp(dxw),
+               stream())
+        # (4) the two 1x1 projections
+        self.cg.conv_backward(prec, dgw, self.gw_src, grads,
+                              {"mode": "f32", "out": d_gup, "accum": d_gup_accum})
+        dx2, acc2 = x.grad_target()
+        self.cx.conv_backward(prec, dxw, [x.src()], grads, {"mode": "f32", "out": dx2, "accum": acc2})
+
+
+# ------------------------------------------------------------------------------------------------
+def _pad_geometry(x1: Act, x2: Act):
+    up_h, up_w = 2 * x1.H, 2 * x1.W
+    dy, dx = x2.H - up_h, x2.W - up_w
+    return up_h, up_w, dy // 2, dx // 2     # F.pad([dx//2, dx-dx//2, dy//2, dy-dy//2]) — layers.py:101
+
+
+class UpStage:
+    """Up (layers.py:64-106) and AttentionUp (layers.py:195-255), bilinear=True:
+    [skip (· attention), pad(up(x1))] -> DoubleConv, with the concat/pad/upsample virtual."""
+
+    def __init__(self, m, attention: bool):
+        if not isinstance(m.up, torch.nn.Upsample):
+            raise NotImplementedError("unet HIP path: bilinear=False (ConvTranspose2d up) is not implemented yet")
+        self.dc = DoubleConvStage(m.conv)
+        self.gate = GateStage(m.attention) if attention else None
+
+    def forward(self, prec, x1: Act, x2: Act, training: bool) -> Act:
+        self.x1, self.x2 = x1, x2
+        self.geo = _pad_geometry(x1, x2)
+        up_h, up_w, pt, pl = self.geo
+        if self.gate is not None:
+            self.gate.forward(prec, x1, x2, training)
+            skip = self.gate.gated_src()
+        else:
+            skip = x2.src()
+        srcs = [skip, x1.src_up(up_h, up_w, pt, pl)]
+        return self.dc.forward(prec, srcs, x2.N, x2.H, x2.W, training)
+
+    def backward(self, prec, grads: Grads):
+        x1, x2 = self.x1, self.x2
+        dev = x2.data.device
+        up_h, up_w, pt, pl = self.geo
+        d_up = f32(x2.N, x2.H, x2.W, x1.C, device=dev)
+        if self.gate is not None:
+            d_xs = f32(x2.N, x2.H, x2.W, x2.C, device=dev)
+            self.dc.backward(prec, grads, {"mode": "f32", "out": d_xs, "accum": 0, "out2": d_up, "accum2": 0,
+                                           "split": x2.C})
+            same = (up_h == x2.H and up_w == x2.W and pt == 0 and pl == 0)
+            if same:
+                self.gate.backward(prec, d_xs, grads, d_up, 1)
+            else:
+                d_gup = f32(x2.N, x2.H, x2.W, x1.C, device=dev)
+                self.gate.backward(prec, d_xs, grads, d_gup, 0)
+                gx, acc = x1.grad_target()
+                L.call("unet_upsample_bwd", x1.N, x1.C, x1.H, x1.W, x2.H, x2.W, 0, 0, x2.H, x2.W,
+                       up_scale(x1.H, x2.H), up_scale(x1.W, x2.W), vp(d_gup), vp(gx), acc, stream())
+        else:
+            g2, acc2 = x2.grad_target()
+            self.dc.backward(prec, grads, {"mode": "f32", "out": g2, "accum": acc2, "out2": d_up, "accum2": 0,
+                                           "split": x2.C})
+        gx, acc = x1.grad_target()
+        L.call("unet_upsample_bwd", x1.N, x1.C, x1.H, x1.W, up_h, up_w, pt, pl, x2.H, x2.W,
+               up_scale(x1.H, up_h), up_scale(x1.W, up_w), vp(d_up), vp(gx), acc, stream())
+
+
+class DownStage:
+    """Down: MaxPool2d(2) -> DoubleConv — layers.py:44-61 (the pool is the conv loader's job)."""
+
+    def __init__(self, m):
+        self.dc = DoubleConvStage(m.maxpool_conv[1])
+
+    def forward(self, prec, x: Act, training: bool) -> Act:
+        self.x = x
+        return self.dc.forward(prec, [x.src_pool()], x.N, x.H // 2, x.W // 2, training)
+
+    def backward(self, prec, grads: Grads):
+        g = self.x.grad_zeroed()
+        self.dc.backward(prec, grads, {"mode": "pool", "out": g, "pool_src": self.x.src_pool()})
+
+
+class OutConvStage:
+    """OutConv: 1x1 conv with bias -> fp32 NCHW logits — layers.py:109-123."""
+
+    def __init__(self, m):
+        self.conv = m.conv
+        self.k = self.conv.out_channels
+
+    def forward(self, prec, a: Act) -> torch.Tensor:
+        self.a = a
+        dev = a.data.device
+        out = f32(a.N, self.k, a.H, a.W, device=dev)
+        self.w = self.conv.weight.detach().reshape(self.k, -1).float().contiguous()
+        b = self.conv.bias.detach().float().contiguous()
+        L.call("unet_outconv_fwd", prec.code, a.N, a.H, a.W, a.C, self.k, vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+               int(a.relu), vp(self.w), vp(b), vp(out), stream())
+        return out
+
+    def backward(self, prec, dlogits: torch.Tensor, grads: Grads):
+        a = self.a
+        dev = a.data.device
+        dl = dlogits.float().contiguous()
+        rows = L.load().unet_outconv_rows(a.pixels)
+        part = f32(rows, self.k + 1, max(a.C, self.k), device=dev)
+        g, acc = a.grad_target()
+        L.call("unet_outconv_bwd", prec.code, a.N, a.H, a.W, a.C, self.k, vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+               int(a.relu), vp(self.w), vp(dl), vp(g), acc, vp(part), stream())
+        dw, db = f32(self.k, a.C, 1, 1, device=dev), f32(self.k, device=dev)
+        L.call("unet_outconv_bwd_finalize", vp(part), rows, a.C, self.k, vp(dw), vp(db), 0, stream())
+        grads.put(self.conv.weight, dw)
+        grads.put(self.conv.bias, db)
+
+
+class DSHeadStage:
+    """Deep-supervision head: OutConv on a decoder map, bilinear(align_corners) to the input size —
+    unet.py:170-173, 204-209."""
+
+    def __init__(self, m):
+        self.oc = OutConvStage(m)
+
+    def forward(self, prec, a: Act, H: int, W: int) -> torch.Tensor:
+        lo = self.oc.forward(prec, a)
+        self.lo_shape = lo.shape
+        self.size = (H, W)
+        out = f32(a.N, self.oc.k, H, W, device=lo.device)
+        L.call("unet_resize_nchw", a.N * self.oc.k, a.H, a.W, H, W, up_scale(a.H, H), up_scale(a.W, W), vp(lo),
+               vp(out), stream())
+        return out
+
+    def backward(self, prec, dout: torch.Tensor, grads: Grads):
+        a = self.oc.a
+        H, W = self.size
+        dlo = f32(*self.lo_shape, device=dout.device)
+        dd = dout.float().contiguous()
+        L.call("unet_resize_nchw_bwd", a.N * self.oc.k, a.H, a.W, H, W, up_scale(a.H, H), up_scale(a.W, W), vp(dd),
+               vp(dlo), 0, stream())
+        self.oc.backward(prec, dlo, grads)
+
+
+# ------------------------------------------------------------------------------------------------
+class NetworkPlan:
+    """UNet.forward (unet.py:67-92) / AttentionUNet.forward (unet.py:175-211) as one launch plan."""
+
+    def __init__(self, model, attention: bool):
+        self.model = model
+        self.attention = attention
+        self.inc = DoubleConvStage(model.inc)
+        self.downs = [DownStage(getattr(model, f"down{i}")) for i in range(1, 5)]
+        self.ups = [UpStage(getattr(model, f"up{i}"), attention) for i in range(1, 5)]
+        self.outc = OutConvStage(model.outc)
+        self.ds = attention and getattr(model, "deep_supervision", False)
+        if self.ds:
+            self.heads = [DSHeadStage(model.ds_out1), DSHeadStage(model.ds_out2), DSHeadStage(model.ds_out3)]
+
+    def forward(self, prec: Precision, x: torch.Tensor, training: bool, need_dx: bool):
+        N, C, H, W = x.shape
+        self.x = x
+        self.need_dx = need_dx
+        xs = [self.inc.forward(prec, [_nchw(x)], N, H, W, training, keep=x)]
+        for d in self.downs:
+            xs.append(d.forward(prec, xs[-1], training))
+        self.xs = xs
+        y = xs[4]
+        dec = []
+        for i, u in enumerate(self.ups):
+            y = u.forward(prec, y, xs[3 - i], training)
+            dec.append(y)
+        self.dec = dec     # d4, d3, d2, d1
+        logits = self.outc.forward(prec, y)
+        self.with_ds = self.ds and training
+        if self.with_ds:
+            # [logits, ds1(d2), ds2(d3), ds3(d4)]
+            outs = [logits]
+            for head, a in zip(self.heads, (dec[2], dec[1], dec[0])):
+                outs.append(head.forward(prec, a, H, W))
+            return outs
+        return [logits]
+
+    def backward(self, prec: Precision, gouts, grads: Grads):
+        gl = gouts[0]
+        if gl is None:
+            gl = torch.zeros(self.x.shape[0], self.outc.k, self.x.shape[2], self.x.shape[3], device=self.x.device)
+        self.outc.backward(prec, gl, grads)
+        if self.with_ds:
+            for head, g in zip(self.heads, gouts[1:]):
+                if g is not None:
+                    head.backward(prec, g, grads)
+        for u in reversed(self.ups):
+            u.backward(prec, grads)
+        for d in reversed(self.downs):
+            d.backward(prec, grads)
+        dx = None
+        if self.need_dx:
+            x = self.x
+            N, C, H, W = x.shape
+            gx = f32(N, H, W, C, device=x.device)
+            self.inc.backward(prec, grads, {"mode": "f32", "out": gx, "accum": 0})
+            from .runtime import grad_nhwc_to_nchw
+            dx = grad_nhwc_to_nchw(gx)
+        else:
+            self.inc.backward(prec, grads, None)
+        return dx
+
+
+def _nchw(x: torch.Tensor) -> L.Src:
+    from .runtime import nchw_src
+    return nchw_src(x)
