@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Benchmark: 512x512 CT slices/sec fwd+bwd, AttentionUNet bs=4/GPU (BASELINE.json metric).
+
+One step = the reference's training micro-step (scripts/train.py:127-143) on one synthetic batch per
+GPU: forward -> DiceBCELoss -> backward -> (DDP all-reduce) -> clip_grad_norm_(1.0) -> AdamW.step
+-> zero_grad.  Inputs are generated once and stay resident in HBM.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints one JSON line (value = whole-job images/s, max-over-ranks time).  The line carries
+`roofline` (the dominant kernel, timed live with HIP events on its launch stream) and
+`cpu_baseline` (the CPU oracle timed on a bounded sample on this host, rank 0 at N=1 only).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "unet-segment-pytorch_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense peaks (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+FLOPS_PER_IMAGE = {"attention_unet": 983.4e9, "unet": 957.5e9}   # fwd+bwd, 1ch 512^2
+
+
+def disc_targets(n: int, h: int, w: int, gen: torch.Generator) -> torch.Tensor:
+    """1-3 discs of radius 6-20 px per image (≈0.36 % foreground on average)."""
+    t = torch.zeros(n, h, w, dtype=torch.int64)
+    yy, xx = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+    for i in range(n):
+        for _ in range(int(torch.randint(1, 4, (1,), generator=gen))):
+            cy, cx = int(torch.randint(0, h, (1,), generator=gen)), int(torch.randint(0, w, (1,), generator=gen))
+            r = int(torch.randint(6, 21, (1,), generator=gen))
+            t[i][(yy - cy) ** 2 + (xx - cx) ** 2 <= r * r] = 1
+    return t
+
+
+def cpu_baseline(model_kind: str, size: int, batch: int, iters: int) -> dict:
+    """Time the CPU oracle (fp32 NCHW ATen restatement of the reference) on a bounded sample."""
+    sys.path.insert(0, str(ROOT))
+    from oracle import unet_oracle as O
+    from unet.models import AttentionUNet, UNet
+    torch.manual_seed(0)
+    m = AttentionUNet(1, 2) if model_kind == "attention_unet" else UNet(1, 2)
+    p = O.params_from_module(m)
+    g = torch.Generator().manual_seed(99)
+    x = torch.rand(batch, 1, size, size, generator=g) * 2 - 1
+    t = disc_targets(batch, size, size, g)
+    fwd = O.attention_unet_forward if model_kind == "attention_unet" else O.unet_forward
+
+    def one():
+        for v in p.values():
+            if v.grad is not None:
+                v.grad = None
+        loss = O.dice_bce_loss(fwd(p, x, training=True), t)
+        loss.backward()
+
+    one()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        one()
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * iters / dt, 4), "unit": "img/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle/unet_oracle.py fp32 CPU, {model_kind} 1x{size}x{size}, batch {batch}, "
+                      f"1 warm-up + {iters} timed fwd+DiceBCE+bwd iterations ({dt:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="attention_unet", choices=["attention_unet", "unet"])
+    ap.add_argument("--batch", type=int, default=4, help="per-GPU batch")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--probe", default=None, help="kernel family to time live (default: conv_kernel<prec,3,64>)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=1)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from unet._hip.runtime import probe
+    from unet.models import AttentionUNet, UNet
+    from unet.utils.loss import DiceBCELoss
+
+    torch.manual_seed(0)
+    model = (AttentionUNet(1, 2) if args.model == "attention_unet" else UNet(1, 2)).to(dev).train()
+    model.hip_precision = args.precision
+    net = model
+    if world > 1:
+        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False,
+                                                        gradient_as_bucket_view=True, bucket_cap_mb=100)
+    opt = torch.optim.AdamW(model.parameters(), lr=5e-5, weight_decay=1e-4, fused=True)
+    crit = DiceBCELoss()
+    gen = torch.Generator().manual_seed(1234 + rank)
+    x = (torch.rand(args.batch, 1, args.size, args.size, generator=gen) * 2 - 1).to(dev)
+    t = disc_targets(args.batch, args.size, args.size, gen).to(dev)
+    params = list(model.parameters())
+
+    def step():
+        loss = crit(net(x), t)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    target = args.probe or f"conv_kernel<{args.precision},3,64>"
+    probe.enable(target)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    probe.disable()
+    if world > 1:
+        te = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = float(te)
+    ps = probe.summary()
+
+    images = world * args.batch * args.steps
+    value = images / elapsed
+    peak = MFMA_PEAK_TFLOPS[args.precision]
+    achieved = ps["tflops"] or 0.0
+    traffic = None
+    tfile = ROOT / "profiles" / "traffic.json"
+    if tfile.exists():
+        tr = json.loads(tfile.read_text())
+        traffic = tr.get(target)
+    line = {
+        "metric": "512x512 CT slices/sec fwd+bwd, AttentionUNet bs=4/GPU, 1/2/4/8 MI355X",
+        "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision, "data": "synthetic (x~U(-1,1), 1-3 disc masks/img; seeded)",
+        "config": {"workload": f"{args.model} 1x{args.size}x{args.size} train step (fwd+DiceBCE+bwd+clip+AdamW)",
+                   "model": args.model, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                   "image": [1, args.size, args.size], "parallelism": f"dp{world}" if world > 1 else "single"},
+        "whole_step_tflops": round(value * FLOPS_PER_IMAGE[args.model] / 1e12, 2),
+        "roofline": {"kernel": target, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "launches": ps["launches"], "avg_us": round(ps["avg_us"], 2) if ps["avg_us"] else None,
+                     "flops_per_launch": round(ps["flops"] / ps["launches"]) if ps["launches"] else None},
+        "final_loss": round(float(loss), 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.model, args.size, args.cpu_batch, args.cpu_iters)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

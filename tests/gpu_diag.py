@@ -86,10 +86,32 @@ def full(prec="bf16", bs=4, iters=5, attention=True):
           flush=True)
 
 
+def autocast_ref():
+    """Inherent bf16 error: the oracle (ATen) under torch.autocast(bf16) on the GPU vs the fp32 golden."""
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from oracle import unet_oracle as O
+    gm = load_golden("models.pt")
+    for name in ["attention_unet_b8", "unet_b8"]:
+        rec = gm[name]
+        p = {k: (v.cuda().requires_grad_(True) if v.is_floating_point() and "running" not in k else v.cuda())
+             for k, v in rec["init"].items()}
+        fwd = O.unet_forward if rec["kind"] == "unet" else O.attention_unet_forward
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = fwd(p, rec["x"].cuda(), training=True)
+        loss = O.dice_bce_loss(out.float(), rec["t"].cuda())
+        loss.backward()
+        worst = max((float((p[k].grad.cpu() - g).abs().max()) / (float(g.abs().max()) + 1e-12), k)
+                    for k, g in rec["grads"].items())
+        print(f"[autocast-bf16 {name}] logits rel {rel_err(out.float(), rec['outputs'][0]):.1e} maxabs "
+              f"{max_abs(out.float(), rec['outputs'][0]):.2e} loss {float(loss):.6f} dparam {worst[0]:.2e} ({worst[1]})",
+              flush=True)
+
+
 if __name__ == "__main__":
     print(torch.cuda.get_device_name(0), flush=True)
     modules()
     models()
+    autocast_ref()
     if "--full" in sys.argv:
         full("bf16")
         full("fp32", iters=2)

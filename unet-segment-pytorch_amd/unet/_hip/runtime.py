@@ -48,6 +48,57 @@ def get_precision(module: Optional[torch.nn.Module] = None) -> Precision:
 # device plumbing
 # ------------------------------------------------------------------------------------------------
 
+class KernelProbe:
+    """Brackets selected kernel launches with HIP events on the launch stream (used by bench.py for
+    the live roofline of one kernel symbol).  Disabled unless `enable()` was called."""
+
+    def __init__(self):
+        self.target = None
+        self.records = []   # (start_event, end_event, algorithmic_flops)
+
+    def enable(self, target: str):
+        self.target = target
+        self.records = []
+
+    def disable(self):
+        self.target = None
+
+    def reset(self):
+        self.records = []
+
+    def launch(self, name: str, flops: float, fn):
+        if self.target is None or name != self.target:
+            return fn()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = fn()
+        e.record()
+        self.records.append((s, e, flops))
+        return r
+
+    def summary(self):
+        torch.cuda.synchronize()
+        t = sum(s.elapsed_time(e) for s, e, _ in self.records) * 1e-3
+        f = sum(fl for _, _, fl in self.records)
+        n = len(self.records)
+        return {"launches": n, "seconds": t, "flops": f, "avg_us": (t / n * 1e6) if n else None,
+                "tflops": (f / t / 1e12) if t > 0 else None}
+
+
+probe = KernelProbe()
+
+
+def conv_kernel_name(prec: "Precision", ksize: int, cout: int) -> str:
+    """Symbol family chosen by unet_conv's dispatch (csrc/conv.hip dispatch_conv)."""
+    bn = 32 if cout <= 32 else 64
+    return f"conv_kernel<{prec.name},{ksize},{bn}>"
+
+
+def wgrad_kernel_name(prec: "Precision", ksize: int) -> str:
+    return f"wgrad_kernel<{prec.name},{ksize}>"
+
+
 def require_device(t: torch.Tensor, what: str = "input") -> None:
     if not t.is_cuda:
         raise RuntimeError(

@@ -13,7 +13,8 @@ from typing import Dict, List, Optional
 import torch
 
 from . import lib as L
-from .runtime import Act, Precision, f32, pack_weight, stream, up_scale, vp
+from .runtime import (Act, Precision, conv_kernel_name, f32, pack_weight, probe, stream, up_scale, vp,
+                      wgrad_kernel_name)
 
 
 def _conv_desc(prec: Precision, N: int, H: int, W: int, cin: int, cout: int, k: int, srcs: List[L.Src],
@@ -72,7 +73,8 @@ class ConvBN:
             mt = L.load().unet_conv_mtiles(N, H, W)
             stats = f32(2, mt, self.cout, device=dev)
             d.stats = stats.data_ptr()
-        L.call("unet_conv", d, stream())
+        probe.launch(conv_kernel_name(prec, self.k, self.cout), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
+                     lambda: L.call("unet_conv", d, stream()))
         mean = invstd = None
         if use_batch:
             mean = f32(self.cout, device=dev)
@@ -130,7 +132,8 @@ class ConvBN:
         ws_bytes = L.load().unet_wgrad_workspace(wd)
         ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
         wd.workspace = ws.data_ptr()
-        L.call("unet_conv_wgrad", wd, stream())
+        probe.launch(wgrad_kernel_name(prec, self.k), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
+                     lambda: L.call("unet_conv_wgrad", wd, stream()))
         grads.put(self.conv.weight, dw)
         if dgrad is None:
             return
@@ -148,7 +151,8 @@ class ConvBN:
             o2 = dgrad.get("out2")
             d.out2 = o2.data_ptr() if o2 is not None else None
             d.accum2 = int(dgrad.get("accum2", 0))
-        L.call("unet_conv", d, stream())
+        probe.launch(conv_kernel_name(prec, self.k, self.cin), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
+                     lambda: L.call("unet_conv", d, stream()))
 
 
 # ------------------------------------------------------------------------------------------------
