@@ -128,7 +128,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    target = args.probe or f"conv_kernel<{args.precision},3,64>"
+    target = args.probe or f"conv2_kernel<{args.precision},3,4,2,4,1>"
     probe.enable(target)
     if world > 1:
         dist.barrier()

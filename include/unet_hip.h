@@ -95,6 +95,10 @@ const char* unet_last_error(void);
 int unet_version(void);
 /* number of M tiles (8x16 output pixels) of a conv with this geometry: rows of the stats buffer  */
 int unet_conv_mtiles(int N, int H, int W);
+/* rows of the BN partial-sum buffer (stats = float[2][rows][Cout]) unet_conv will write for d    */
+int unet_conv_stats_rows(const unet_conv_desc* d);
+/* name of the kernel instantiation unet_conv dispatches d to (for profiling / roofline probes)   */
+int unet_conv_variant(const unet_conv_desc* d, char* buf, int len);
 
 /* ---- weights (nn.Conv2d weight OIHW fp32 -> packed operand) -------------------------------- */
 /* replaces the implicit weight read of nn.Conv2d — layers.py:32,35,120,152,158,164            */

@@ -1,0 +1,202 @@
+"""GPU op-level numerics: each HIP entry point (through the C-ABI) against a plain PyTorch fp32
+reference of the same op, on operands that are exactly representable in the kernel's operand type
+(bf16-rounded for the bf16 kernels), so the only difference left is the summation order.
+Shapes are chosen to hit every tile configuration of csrc/conv.hip and csrc/wgrad2.hip, including
+partial tiles and channel counts that are not multiples of the tile sizes."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DT = {"fp32": torch.float32, "bf16": torch.bfloat16}
+
+
+def _lib():
+    from unet._hip import lib as L
+    return L
+
+
+def _rt():
+    from unet._hip import runtime as R
+    return R
+
+
+def _rand(*shape, dt, scale=1.0):
+    return (torch.randn(*shape, device="cuda") * scale).to(dt)
+
+
+def _act_src(y, ab, relu=True, kind=None):
+    L = _lib()
+    s = L.Src()
+    s.kind = L.SRC_ACT if kind is None else kind
+    _, s.H, s.W, s.C = y.shape
+    s.data = y.data_ptr()
+    s.scale = ab[0].data_ptr()
+    s.shift = ab[1].data_ptr()
+    s.relu = int(relu)
+    return s
+
+
+def _act_ref(y, ab, relu=True):
+    a = y.float() * ab[0] + ab[1]
+    return a.clamp_min(0) if relu else a
+
+
+def _conv(prec, srcs, N, H, W, cin, w, k, out_mode, **kw):
+    L, R = _lib(), _rt()
+    P = R.BF16 if prec == "bf16" else R.FP32
+    transpose = kw.pop("transpose", False)
+    cout = w.shape[1] if transpose else w.shape[0]
+    wp = R.pack_weight(w, P, transpose=transpose)
+    d = L.ConvDesc()
+    d.dtype = P.code
+    d.N, d.H, d.W, d.Cin, d.Cout, d.ksize = N, H, W, cin, cout, k
+    d.nsrc = len(srcs)
+    for i, s in enumerate(srcs):
+        d.src[i] = s
+    d.weight = wp.data_ptr()
+    d.out_mode = out_mode
+    for key, v in kw.items():
+        setattr(d, key, v)
+    L.call("unet_conv", d, R.stream())
+    torch.cuda.synchronize()
+    return d
+
+
+CONV_SHAPES = [  # (N, H, W, Cin, Cout) — tile configs: BN 32/64/128, TH 8/16, partial tiles
+    (2, 16, 16, 32, 32), (1, 24, 40, 64, 64), (2, 33, 20, 96, 128), (4, 64, 64, 64, 128), (1, 8, 24, 128, 256),
+    (2, 20, 36, 40, 48),
+]
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+@pytest.mark.parametrize("k", [3, 1])
+def test_conv_fwd_act(prec, shape, k):
+    L = _lib()
+    N, H, W, cin, cout = shape
+    dt = DT[prec]
+    torch.manual_seed(0)
+    y = _rand(N, H, W, cin, dt=dt)
+    ab = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2])
+    w = (torch.randn(cout, cin, k, k, device="cuda") * 0.1).to(dt).float()
+    out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
+    st = torch.empty(2, 4096, cout, device="cuda")
+    _conv(prec, [_act_src(y, ab)], N, H, W, cin, w, k, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
+    x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2)
+    ref = F.conv2d(x, w, padding=k // 2).permute(0, 2, 3, 1)
+    tol = 2e-2 if prec == "bf16" else 1e-4
+    assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max()), (out.float() - ref).abs().max()
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("shape", [(2, 16, 16, 32, 64), (1, 21, 30, 64, 128), (2, 8, 8, 128, 64)])
+def test_conv_fwd_pool_and_up_concat(prec, shape):
+    """down.0 (max-pool of ACT) and up.0 ([gated skip, pad(up(ACT))]) loaders."""
+    L = _lib()
+    N, H, W, cin, cout = shape
+    dt = DT[prec]
+    torch.manual_seed(1)
+    # pool
+    ys = _rand(N, 2 * H + 1, 2 * W, cin, dt=dt)
+    ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * 0.1).to(dt).float()
+    out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
+    _conv(prec, [_act_src(ys, ab, kind=L.SRC_POOL_ACT)], N, H, W, cin, w, 3, L.OUT_Y, out=out.data_ptr())
+    x = F.max_pool2d(_act_ref(ys, ab).permute(0, 3, 1, 2), 2)
+    ref = F.conv2d(x.to(dt).float(), w, padding=1).permute(0, 2, 3, 1)
+    tol = 2e-2 if prec == "bf16" else 1e-4
+    assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max())
+    # concat [skip * sigmoid(gate), pad(up(act(dec)))]
+    cs = cin // 2
+    skip = _rand(N, H, W, cs, dt=dt)
+    abs_ = torch.stack([torch.rand(cs, device="cuda") + 0.5, torch.randn(cs, device="cuda") * 0.1])
+    dec = _rand(N, (H - 1) // 2, W // 2, cin - cs, dt=dt)
+    abd = torch.stack([torch.rand(cin - cs, device="cuda") + 0.5, torch.randn(cin - cs, device="cuda") * 0.1])
+    p = torch.randn(N, H, W, device="cuda")
+    pab = torch.tensor([0.7, -0.1], device="cuda")
+    s0 = _act_src(skip, abs_)
+    s0.gate_p, s0.gate_ab = p.data_ptr(), pab.data_ptr()
+    up_h, up_w = 2 * dec.shape[1], 2 * dec.shape[2]
+    s1 = _act_src(dec, abd, kind=L.SRC_UP_ACT)
+    R = _rt()
+    s1.up_h, s1.up_w, s1.pad_t, s1.pad_l = up_h, up_w, (H - up_h) // 2, (W - up_w) // 2
+    s1.sh, s1.sw = R.up_scale(dec.shape[1], up_h), R.up_scale(dec.shape[2], up_w)
+    _conv(prec, [s0, s1], N, H, W, cin, w, 3, L.OUT_Y, out=out.data_ptr())
+    xs = _act_ref(skip, abs_).permute(0, 3, 1, 2) * torch.sigmoid(p * 0.7 - 0.1)[:, None]
+    xu = F.interpolate(_act_ref(dec, abd).permute(0, 3, 1, 2), size=(up_h, up_w), mode="bilinear", align_corners=True)
+    dyy, dxx = H - up_h, W - up_w
+    xu = F.pad(xu, [dxx // 2, dxx - dxx // 2, dyy // 2, dyy - dyy // 2])
+    ref = F.conv2d(torch.cat([xs, xu], 1).to(dt).float(), w, padding=1).permute(0, 2, 3, 1)
+    assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max())
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("shape", [(2, 16, 16, 64, 32), (1, 24, 40, 128, 64), (2, 18, 20, 64, 128)])
+def test_conv_dgrad_split_and_pool(prec, shape):
+    L = _lib()
+    N, H, W, cin, cout = shape     # forward conv cin -> cout; dgrad maps dy[cout] -> dx[cin]
+    dt = DT[prec]
+    torch.manual_seed(2)
+    dy = _rand(N, H, W, cout, dt=dt)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * 0.1).to(dt).float()
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    split = cin // 4 * 2
+    o1 = torch.full((N, H, W, split), 1.0, device="cuda")
+    o2 = torch.empty(N, H, W, cin - split, device="cuda")
+    _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
+          split=split, accum=1, accum2=0)
+    tol = 2e-2 if prec == "bf16" else 1e-4
+    got = torch.cat([o1 - 1.0, o2], -1)
+    assert (got - ref).abs().max() <= tol * (1 + ref.abs().max())
+    # pool-bwd routing: gradient of maxpool(act(ys)) at the pooled resolution
+    ys = _rand(N, 2 * H, 2 * W + 1, cin, dt=dt)
+    ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
+    da = torch.zeros(N, 2 * H, 2 * W + 1, cin, device="cuda")
+    _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_POOL_BWD, transpose=True, out=da.data_ptr(),
+          pool_src=_act_src(ys, ab))
+    a = _act_ref(ys, ab).permute(0, 3, 1, 2).requires_grad_(True)
+    F.max_pool2d(a, 2).backward(ref.permute(0, 3, 1, 2))
+    assert (da.permute(0, 3, 1, 2) - a.grad).abs().max() <= tol * (1 + ref.abs().max())
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("shape", [(2, 16, 16, 64, 64), (1, 24, 40, 32, 128), (2, 40, 36, 128, 256),
+                                   (4, 32, 32, 96, 64)])
+@pytest.mark.parametrize("k", [3, 1])
+@pytest.mark.parametrize("kind", ["act", "pool"])
+def test_conv_wgrad(prec, shape, k, kind):
+    L, R = _lib(), _rt()
+    P = R.BF16 if prec == "bf16" else R.FP32
+    N, H, W, cin, cout = shape
+    dt = DT[prec]
+    torch.manual_seed(3)
+    dy = _rand(N, H, W, cout, dt=dt)
+    ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
+    if kind == "act":
+        y = _rand(N, H, W, cin, dt=dt)
+        src = _act_src(y, ab)
+        x = _act_ref(y, ab).permute(0, 3, 1, 2)
+    else:
+        y = _rand(N, 2 * H, 2 * W, cin, dt=dt)
+        src = _act_src(y, ab, kind=L.SRC_POOL_ACT)
+        x = F.max_pool2d(_act_ref(y, ab).permute(0, 3, 1, 2), 2)
+    x = x.to(dt).float()
+    ref = torch.nn.grad.conv2d_weight(x, (cout, cin, k, k), dy.float().permute(0, 3, 1, 2), padding=k // 2)
+    wd = L.WgradDesc()
+    wd.dtype = P.code
+    wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = N, H, W, cin, cout, k, 1
+    wd.src[0] = src
+    wd.dy = dy.data_ptr()
+    dw = torch.empty(cout, cin, k, k, device="cuda")
+    wd.dw = dw.data_ptr()
+    ws = torch.empty(max(L.load().unet_wgrad_workspace(wd), 16), dtype=torch.uint8, device="cuda")
+    wd.workspace = ws.data_ptr()
+    L.call("unet_conv_wgrad", wd, R.stream())
+    torch.cuda.synchronize()
+    tol = 1e-3 if prec == "bf16" else 1e-4
+    assert (dw - ref).abs().max() <= tol * (1 + ref.abs().max()), float((dw - ref).abs().max())

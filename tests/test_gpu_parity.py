@@ -82,16 +82,33 @@ def test_model_fp32_vs_golden(golden_models, name):
     assert max_abs(ev, rec["eval_logits"]) <= 1e-4 * (1 + float(rec["eval_logits"].abs().max()))
 
 
-def test_model_bf16_vs_golden(golden_models):
+@pytest.mark.parametrize("name", ["attention_unet_b8", "unet_b8"])
+def test_model_bf16_vs_golden(golden_models, name):
+    """bf16 operand mode: no worse than the reference's own network run under torch.autocast(bf16)
+    (the oracle's ATen ops on the GPU), measured against the same fp32 golden logits/loss.  On this
+    tiny random-init net the inherent bf16 error is large (logits rel-L2 ~4-9 %), so a fixed
+    tolerance would be meaningless; the bound is relative to PyTorch's own bf16 execution."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from oracle import unet_oracle as O
     from unet.utils.loss import DiceBCELoss
-    rec = golden_models["attention_unet_b8"]
+    rec = golden_models[name]
     m = build_model(rec)
     m.hip_precision = "bf16"
     out = m(rec["x"].cuda())
     loss = DiceBCELoss()(out, rec["t"].cuda())
     loss.backward()
-    assert rel_err(out, rec["outputs"][0]) <= 2e-2
-    assert abs(float(loss) - float(rec["loss"])) <= 2e-2 * abs(float(rec["loss"]))
+    p = {k: v.cuda() for k, v in rec["init"].items()}
+    fwd = O.unet_forward if rec["kind"] == "unet" else O.attention_unet_forward
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        ac = fwd(p, rec["x"].cuda(), training=True).float()
+    ac_loss = O.dice_bce_loss(ac, rec["t"].cuda())
+    ref = rec["outputs"][0]
+    e_ours, e_torch = rel_err(out, ref), rel_err(ac, ref)
+    assert e_ours <= 1.5 * e_torch + 1e-2, (e_ours, e_torch)
+    l_ref = float(rec["loss"])
+    assert abs(float(loss) - l_ref) <= 1.5 * abs(float(ac_loss) - l_ref) + 2e-3 * abs(l_ref)
 
 
 @pytest.mark.parametrize("name", ["dice_bce", "dice", "balanced_ce", "dice_bce_w"])

@@ -1,75 +1,67 @@
-// conv.hip — LDS-tiled direct convolution on MFMA for gfx950 (fwd + dgrad), weight packing.
+// conv.hip — LDS-halo direct convolution on MFMA for gfx950 (fwd + dgrad) and weight packing.
 //
 // Replaces nn.Conv2d(k=3, pad=1, bias=False) / nn.Conv2d(k=1, bias=False) of
-// unet/models/layers.py:32,35,152,158 and their input-gradient.  One workgroup computes an
-// 8x16-pixel x BN-channel output tile of one image:
-//   * the (8+2)x(16+2) input halo for a 64-byte channel chunk is gathered ONCE into LDS through
-//     src_gather() (BN-apply+ReLU, max-pool, bilinear-up, pad, concat and attention multiply are
-//     applied on the way in), and re-used by all 9 taps;
-//   * the packed weights of the chunk ([tap][co][ci], 64-B rows) are staged next to it;
-//   * 4 waves (2 x 2) run v_mfma_f32_16x16x32_bf16 (bf16) or v_mfma_f32_16x16x4_f32 (exact fp32
-//     parity mode) over taps x chunk;
-//   * the epilogue stores y NHWC and per-tile BN partial sums (train-mode BatchNorm stats), or, for
-//     dgrad, fp32 gradients (optionally split across a channel concat, or routed through the 2x2
-//     max-pool argmax).
-#include "src_gather.h"
+// unet/models/layers.py:32,35,152,158 and the input-gradient half of their convolution_backward.
+//
+// One workgroup (WM x WN waves) computes a TH x 16-pixel x BN-channel output tile of one image.
+//  * Input ("A"): per 64-byte channel chunk, the (TH+2) x 18 halo is gathered ONCE into LDS and
+//    re-used by all 9 taps.  The gather applies the virtual-activation transform of the source
+//    (BN-apply+ReLU, 2x2 max-pool, bilinear-up + pad, concat, attention multiply; src_gather.h), and
+//    is software-pipelined: the raw loads of chunk c+1 are issued before chunk c's MFMAs and only
+//    transformed + written to the second LDS buffer after them (one barrier per chunk).
+//  * Weights ("B"): packed fragment-major ([n-tile][chunk][tap][lane][16 B]) so each MFMA operand is
+//    one coalesced 1 KiB wave load straight from L2 into VGPRs, prefetched two taps ahead; no LDS.
+//  * MFMA: v_mfma_f32_16x16x32_bf16 (bf16) or v_mfma_f32_16x16x4_f32 (exact fp32 parity mode).
+//  * Epilogue: y (NHWC) + per-tile BN partial sums, or fp32 gradients (channel split for the concat,
+//    or routed through the 2x2 max-pool argmax).
+#include <stdio.h>
+#include "halo_items.h"
 
 namespace unet {
 
-constexpr int TH = 8, TW = 16, BM = TH * TW, NTHR = 256;
-
-template <typename T> struct Mma;
-template <> struct Mma<bf16> {
-  static constexpr int KC = 32;     // channels per staged chunk (64 bytes)
-  static constexpr int KSTEP = 32;  // K of one MFMA
-  static constexpr int E = 8;       // operand elements per lane
-  typedef bf16x8 frag;
-  __device__ static __forceinline__ frag load(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
-  __device__ static __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  }
-};
-template <> struct Mma<float> {
-  static constexpr int KC = 16;
-  static constexpr int KSTEP = 4;
-  static constexpr int E = 1;
-  typedef float frag;
-  __device__ static __forceinline__ frag load(const float* p) { return *p; }
-  __device__ static __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-};
-
-template <typename T> __host__ __device__ constexpr int kc_of() { return sizeof(T) == 2 ? 32 : 16; }
-static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
-__device__ __forceinline__ int round_up_d(int a, int b) { return (a + b - 1) / b * b; }
+constexpr int CTW = 16;          // tile width in pixels
+constexpr int PACK_NPAD = 128;   // packed rows padded to the largest BN
 
 // ------------------------------------------------------------------------------------------------
-// forward / dgrad kernel
-// ------------------------------------------------------------------------------------------------
-template <typename T, int KS, int BN>
-__global__ __launch_bounds__(NTHR) void conv_kernel(const unet_conv_desc d, int tiles_w, int tiles_h, int mtiles) {
+template <typename T, int KS, int WM, int WN, int NTN, int RAW>
+__global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_desc d, int tiles_w, int tiles_h,
+                                                             int mtiles, int nchunks) {
   using M = Mma<T>;
+  constexpr int NT = 64 * WM * WN;
   constexpr int KC = M::KC, VEC = Vec<T>::N, NV = KC / VEC;
+  constexpr int TH = 4 * WM, BN = WN * NTN * 16;
   constexpr int HALO = (KS == 3) ? 1 : 0;
-  constexpr int HWID = TW + 2 * HALO, HHGT = TH + 2 * HALO, HP = HWID * HHGT;
-  constexpr int RS = KC + 16 / (int)sizeof(T);  // padded LDS row (elements): 80 bytes
+  constexpr int HWID = CTW + 2 * HALO, HHGT = TH + 2 * HALO, HP = HWID * HHGT;
+  constexpr int RS = KC + 16 / (int)sizeof(T);  // 80-byte LDS rows
   constexpr int TAPS = KS * KS;
-  constexpr int NTN = BN / 32;                  // 16-wide n-tiles per wave (2 waves along N)
-  __shared__ __attribute__((aligned(16))) T lds[(HP + TAPS * BN) * RS];
-  T* lds_x = lds;
-  T* lds_w = lds + HP * RS;
+  constexpr int ITEMS = (HP * NV + NT - 1) / NT;
+  constexpr int E16 = 16 / (int)sizeof(T);
+  static_assert(NT % NV == 0, "thread->channel-vector mapping must be fixed");
+  __shared__ __attribute__((aligned(16))) T lds[2 * HP * RS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int mt = blockIdx.x;
   const int tw_i = mt % tiles_w;
   const int t2 = mt / tiles_w;
   const int th_i = t2 % tiles_h;
   const long long n = t2 / tiles_h;
-  const int h0 = th_i * TH, w0 = tw_i * TW;
+  const int h0 = th_i * TH, w0 = tw_i * CTW;
   const int co0 = blockIdx.y * BN;
-  const int Cin_pad = round_up_d(d.Cin, KC);
+
+  // this thread's halo items: item k covers halo vector (tid + k*NT); its channel vector v is the same
+  // for every k and every chunk (NT % NV == 0)
+  const int v = tid % NV;
+  auto item_hp = [&](int k) { return (tid + k * NT) / NV; };
+  auto item_y = [&](int k) { return h0 + item_hp(k) / HWID - HALO; };
+  auto item_x = [&](int k) { return w0 + item_hp(k) % HWID - HALO; };
+
+  // weight fragments: [ntile][chunk][tap][lane][16B]
+  const uint4* wbase = reinterpret_cast<const uint4*>(d.weight);
+  const int ntile0 = co0 / 16 + wn * NTN;
+  auto bptr = [&](int j, int c, int t) -> const uint4* {
+    return wbase + ((((size_t)(ntile0 + j) * nchunks + c) * TAPS + t) * 64 + lane);
+  };
 
   f32x4 acc[4][NTN];
 #pragma unroll
@@ -77,48 +69,104 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(const unet_conv_desc d, int 
 #pragma unroll
     for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int c0 = 0; c0 < d.Cin; c0 += KC) {
-    // ---- stage the input halo (transformed) ----
-    for (int it = tid; it < HP * NV; it += NTHR) {
-      const int hp = it / NV, v = it % NV;
-      const int hy = h0 + hp / HWID - HALO, hx = w0 + hp % HWID - HALO;
-      float vals[VEC];
-      src_gather<T>(d.src, d.nsrc, d.Cin, d.H, d.W, n, hy, hx, c0 + v * VEC, vals);
-      store_vec<T>(lds_x + hp * RS + v * VEC, vals);
-    }
-    // ---- stage the packed weights of this chunk ----
-    for (int it = tid; it < TAPS * BN * NV; it += NTHR) {
-      const int row = it / NV, v = it % NV;
-      const int tap = row / BN, col = row % BN;
-      const int co = co0 + col;
-      uint4 q = make_uint4(0, 0, 0, 0);
-      if (co < d.Cout)
-        q = *reinterpret_cast<const uint4*>((const T*)d.weight + ((size_t)co * TAPS + tap) * Cin_pad + c0 + v * VEC);
-      *reinterpret_cast<uint4*>(lds_w + (tap * BN + col) * RS + v * VEC) = q;
-    }
-    __syncthreads();
+  SrcView sv;
+  float sc[VEC], sf[VEC];
+  Item<RAW> item;
+
+  // ---- prologue: chunk 0 into buffer 0 ----
+  make_view<T>(d, v * VEC, sv, sc, sf);
 #pragma unroll
-    for (int tap = 0; tap < TAPS; ++tap) {
-      const int dy = tap / KS, dx = tap % KS;
+  for (int k = 0; k < ITEMS; ++k) {
+    const int hp = item_hp(k);
+    if (hp < HP) {
+      item_issue<T, RAW>(sv, d.H, d.W, n, item_y(k), item_x(k), 1, item);
+      float vals[VEC];
+      item_finish<T, RAW>(d, sv, sc, sf, n, item_y(k), item_x(k), v * VEC, item, vals);
+      store_vec<T>(lds + hp * RS + v * VEC, vals);
+    }
+  }
+  uint4 B[2][NTN];
+#pragma unroll
+  for (int j = 0; j < NTN; ++j) B[0][j] = *bptr(j, 0, 0);
+  __syncthreads();
+
+  for (int c = 0; c < nchunks; ++c) {
+    const T* xb = lds + (c & 1) * HP * RS;
+    T* xn = lds + ((c & 1) ^ 1) * HP * RS;
+    const bool has_next = c + 1 < nchunks;
+    const int cn = (c + 1) * KC + v * VEC;
+    if (has_next) make_view<T>(d, cn, sv, sc, sf);
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t) {
+      // B fragments one tap ahead (crossing into the next chunk)
+      const int tt = t + 1;
+      if (tt < TAPS) {
+#pragma unroll
+        for (int j = 0; j < NTN; ++j) B[tt & 1][j] = *bptr(j, c, tt);
+      } else if (has_next) {
+#pragma unroll
+        for (int j = 0; j < NTN; ++j) B[tt & 1][j] = *bptr(j, c + 1, tt - TAPS);
+      }
+      // next chunk's halo: item k issued at tap 3k, finished (transform + LDS write) at tap 3k+2
+      if constexpr (TAPS == 9) {
+        if (has_next && t % 3 == 0 && t / 3 < ITEMS) {
+          const int k = t / 3;
+          item_issue<T, RAW>(sv, d.H, d.W, n, item_y(k), item_x(k), item_hp(k) < HP, item);
+        }
+      }
+      const int dy = t / KS, dx = t % KS;
 #pragma unroll
       for (int ks = 0; ks < KC / M::KSTEP; ++ks) {
+        typename M::frag a[4];
         const int kofs = ks * M::KSTEP + (lane >> 4) * M::E;
-        typename M::frag a[4], b[NTN];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = M::load(lds_x + ((wm * 4 + i + dy) * HWID + (lane & 15) + dx) * RS + kofs);
+        for (int i = 0; i < 4; ++i) a[i] = M::load(xb + ((wm * 4 + i + dy) * HWID + (lane & 15) + dx) * RS + kofs);
 #pragma unroll
-        for (int j = 0; j < NTN; ++j) b[j] = M::load(lds_w + (tap * BN + wn * (BN / 2) + j * 16 + (lane & 15)) * RS + kofs);
+        for (int j = 0; j < NTN; ++j) {
+          typename M::frag b;
+          const uint4 q = B[t & 1][j];
+          if constexpr (sizeof(T) == 2) b = __builtin_bit_cast(bf16x8, q);
+          else b = __uint_as_float(ks == 0 ? q.x : ks == 1 ? q.y : ks == 2 ? q.z : q.w);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i) acc[i][j] = M::mma(a[i], b, acc[i][j]);
+        }
+      }
+      if constexpr (TAPS == 9) {
+        if (has_next && t % 3 == 2 && t / 3 < ITEMS) {
+          const int k = t / 3;
+          const int hp = item_hp(k);
+          if (hp < HP) {
+            float vals[VEC];
+            item_finish<T, RAW>(d, sv, sc, sf, n, item_y(k), item_x(k), cn, item, vals);
+            store_vec<T>(xn + hp * RS + v * VEC, vals);
+          }
+        }
+      }
+    }
+    // TAPS is odd: the next chunk's tap-0 fragments were prefetched into slot 1
+    if (has_next) {
 #pragma unroll
-          for (int j = 0; j < NTN; ++j) acc[i][j] = M::mma(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < NTN; ++j) B[0][j] = B[1][j];
+    }
+    if constexpr (TAPS == 1) {
+      if (has_next) {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+          const int hp = item_hp(k);
+          if (hp < HP) {
+            item_issue<T, RAW>(sv, d.H, d.W, n, item_y(k), item_x(k), 1, item);
+            float vals[VEC];
+            item_finish<T, RAW>(d, sv, sc, sf, n, item_y(k), item_x(k), cn, item, vals);
+            store_vec<T>(xn + hp * RS + v * VEC, vals);
+          }
+        }
       }
     }
     __syncthreads();
   }
 
   // ---- epilogue ----
-  // acc[i][j][r] (lane l): pixel (h0 + 4*wm + i, w0 + 4*(l>>4) + r), channel co0 + wn*BN/2 + 16j + (l&15)
+  // acc[i][j][r] (lane l): pixel (h0 + 4*wm + i, w0 + 4*(l>>4) + r), channel co0 + (wn*NTN + j)*16 + (l&15)
   const int ow_base = w0 + 4 * (lane >> 4);
   if (d.out_mode == UNET_OUT_Y) {
     T* y = (T*)d.out;
@@ -130,22 +178,21 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(const unet_conv_desc d, int 
       const int oh = h0 + wm * 4 + i;
 #pragma unroll
       for (int j = 0; j < NTN; ++j) {
-        const int co = co0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ow = ow_base + r;
           if (oh < d.H && ow < d.W && co < d.Cout) {
-            const float v = acc[i][j][r];
-            const T tv = from_f<T>(v);
-            y[((n * d.H + oh) * (long long)d.W + ow) * d.Cout + co] = tv;
-            s[j] += v;
-            ss[j] += v * v;
+            const float val = acc[i][j][r];
+            y[((n * d.H + oh) * (long long)d.W + ow) * d.Cout + co] = from_f<T>(val);
+            s[j] += val;
+            ss[j] += val * val;
           }
         }
       }
     }
     if (d.stats) {
-      float* red = reinterpret_cast<float*>(lds);  // [2 wm][BN][2]
+      float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
 #pragma unroll
       for (int j = 0; j < NTN; ++j) {
         s[j] += __shfl_xor(s[j], 16, 64);
@@ -153,7 +200,7 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(const unet_conv_desc d, int 
         ss[j] += __shfl_xor(ss[j], 16, 64);
         ss[j] += __shfl_xor(ss[j], 32, 64);
         if (lane < 16) {
-          const int col = wn * (BN / 2) + j * 16 + lane;
+          const int col = (wn * NTN + j) * 16 + lane;
           red[(wm * BN + col) * 2 + 0] = s[j];
           red[(wm * BN + col) * 2 + 1] = ss[j];
         }
@@ -162,8 +209,11 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(const unet_conv_desc d, int 
       if (tid < BN) {
         const int co = co0 + tid;
         if (co < d.Cout) {
-          d.stats[(size_t)mt * d.Cout + co] = red[tid * 2] + red[(BN + tid) * 2];
-          d.stats[((size_t)mtiles + mt) * d.Cout + co] = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
+          float a = 0.f, b = 0.f;
+#pragma unroll
+          for (int w = 0; w < WM; ++w) { a += red[(w * BN + tid) * 2]; b += red[(w * BN + tid) * 2 + 1]; }
+          d.stats[(size_t)mt * d.Cout + co] = a;
+          d.stats[((size_t)mtiles + mt) * d.Cout + co] = b;
         }
       }
     }
@@ -176,25 +226,25 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(const unet_conv_desc d, int 
       const int oh = h0 + wm * 4 + i;
 #pragma unroll
       for (int j = 0; j < NTN; ++j) {
-        const int co = co0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ow = ow_base + r;
           if (oh < d.H && ow < d.W && co < d.Cout) {
             const long long pix = (n * d.H + oh) * (long long)d.W + ow;
-            const float v = acc[i][j][r];
+            const float val = acc[i][j][r];
             if (co < d.split) {
               float* p = o1 + pix * d.split + co;
-              *p = d.accum ? *p + v : v;
+              *p = d.accum ? *p + val : val;
             } else {
               float* p = o2 + pix * c2 + (co - d.split);
-              *p = d.accum2 ? *p + v : v;
+              *p = d.accum2 ? *p + val : val;
             }
           }
         }
       }
     }
-  } else {  // UNET_OUT_POOL_BWD: gradient w.r.t. the pooled map -> 2x2 argmax of ACT(pool_src)
+  } else {  // UNET_OUT_POOL_BWD
     const unet_src& ps = d.pool_src;
     float* da = (float*)d.out;
     const T* ysrc = (const T*)ps.data;
@@ -203,18 +253,18 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(const unet_conv_desc d, int 
       const int oh = h0 + wm * 4 + i;
 #pragma unroll
       for (int j = 0; j < NTN; ++j) {
-        const int co = co0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ow = ow_base + r;
           if (oh < d.H && ow < d.W && co < d.Cout) {
-            const float sc = ps.scale[co], sf = ps.shift[co];
+            const float scv = ps.scale[co], sfv = ps.shift[co];
             float best = -INFINITY;
             int bq = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const long long sp = (n * ps.H + 2 * oh + (q >> 1)) * (long long)ps.W + 2 * ow + (q & 1);
-              float a = to_f(ysrc[sp * d.Cout + co]) * sc + sf;
+              float a = to_f(ysrc[sp * d.Cout + co]) * scv + sfv;
               if (ps.relu) a = fmaxf(a, 0.f);
               if (a > best || a != a) { best = a; bq = q; }
             }
@@ -227,262 +277,107 @@ __global__ __launch_bounds__(NTHR) void conv_kernel(const unet_conv_desc d, int 
   }
 }
 
-template <typename T, int KS, int BN>
-static int launch_conv(const unet_conv_desc* d, hipStream_t st) {
-  const int tw = cdiv(d->W, TW), th = cdiv(d->H, TH);
+// ------------------------------------------------------------------------------------------------
+// configuration choice (host)
+// ------------------------------------------------------------------------------------------------
+struct ConvCfg {
+  int wm, wn, ntn, raw;
+  const char* name;
+};
+
+static ConvCfg pick_cfg(const unet_conv_desc* d) {
+  ConvCfg c;
+  c.raw = 1;
+  for (int i = 0; i < d->nsrc; ++i)
+    if (d->src[i].kind == UNET_SRC_POOL_ACT || d->src[i].kind == UNET_SRC_UP_ACT) c.raw = 4;
+  const long long tiles16 = (long long)d->N * cdiv(d->H, 16) * cdiv(d->W, CTW);
+  if (d->Cout <= 32) {
+    c.wm = 2; c.wn = 2; c.ntn = 1;
+  } else if (d->Cout <= 64) {
+    if (tiles16 >= 256) { c.wm = 4; c.wn = 2; c.ntn = 2; }
+    else { c.wm = 2; c.wn = 2; c.ntn = 2; }
+  } else {
+    if (c.raw == 1 && tiles16 * cdiv(d->Cout, 128) >= 256) { c.wm = 4; c.wn = 2; c.ntn = 4; }
+    else { c.wm = 2; c.wn = 4; c.ntn = 2; }
+  }
+  return c;
+}
+
+template <typename T, int KS, int WM, int WN, int NTN, int RAW>
+static int launch_conv2(const unet_conv_desc* d, hipStream_t st) {
+  constexpr int TH = 4 * WM, BN = WN * NTN * 16;
+  const int tw = cdiv(d->W, CTW), th = cdiv(d->H, TH);
   const int mt = d->N * tw * th;
+  const int kc = Mma<T>::KC;
   dim3 grid(mt, cdiv(d->Cout, BN));
-  hipLaunchKernelGGL((conv_kernel<T, KS, BN>), grid, dim3(NTHR), 0, st, *d, tw, th, mt);
+  hipLaunchKernelGGL((conv2_kernel<T, KS, WM, WN, NTN, RAW>), grid, dim3(64 * WM * WN), 0, st, *d, tw, th, mt,
+                     cdiv(d->Cin, kc));
   return check_launch("conv");
+}
+
+template <typename T, int KS, int RAW>
+static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t st) {
+  if (c.wm == 2 && c.wn == 2 && c.ntn == 1) return launch_conv2<T, KS, 2, 2, 1, RAW>(d, st);
+  if (c.wm == 4 && c.wn == 2 && c.ntn == 2) return launch_conv2<T, KS, 4, 2, 2, RAW>(d, st);
+  if (c.wm == 2 && c.wn == 2 && c.ntn == 2) return launch_conv2<T, KS, 2, 2, 2, RAW>(d, st);
+  if (c.wm == 4 && c.wn == 2 && c.ntn == 4) return launch_conv2<T, KS, 4, 2, 4, RAW>(d, st);
+  return launch_conv2<T, KS, 2, 4, 2, RAW>(d, st);
+}
+
+template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
+
+// the pipelined kernel needs every source channel vector to be one aligned 16-byte load
+static bool fast_eligible(const unet_conv_desc* d) {
+  const int vec = d->dtype == UNET_BF16 ? 8 : 4;
+  for (int i = 0; i < d->nsrc; ++i)
+    if (d->src[i].kind == UNET_SRC_NCHW_F32 || d->src[i].C % vec) return false;
+  return true;
 }
 
 template <typename T>
 static int dispatch_conv(const unet_conv_desc* d, hipStream_t st) {
-  if (d->ksize == 3) {
-    if (d->Cout <= 32) return launch_conv<T, 3, 32>(d, st);
-    return launch_conv<T, 3, 64>(d, st);
-  }
-  if (d->Cout <= 32) return launch_conv<T, 1, 32>(d, st);
-  return launch_conv<T, 1, 64>(d, st);
+  if (!fast_eligible(d)) return dispatch_generic<T>(d, st);
+  const ConvCfg c = pick_cfg(d);
+  if (d->ksize == 3) return c.raw == 4 ? dispatch_cfg<T, 3, 4>(d, c, st) : dispatch_cfg<T, 3, 1>(d, c, st);
+  return c.raw == 4 ? dispatch_cfg<T, 1, 4>(d, c, st) : dispatch_cfg<T, 1, 1>(d, c, st);
 }
 
 // ------------------------------------------------------------------------------------------------
-// weight gradient: dW[co][tap][ci] = sum_pix dy[pix][co] * X[pix + tap][ci]
-// Split-K over pixel tiles; each block writes an fp32 slab, reduced in a fixed order afterwards.
-// ------------------------------------------------------------------------------------------------
-constexpr int WG_BCO = 64;
-
-template <typename T> struct WgFrag;
-template <> struct WgFrag<bf16> {
-  // A/B operand with K on the LDS ROW axis (pixels) and M/N on the column axis (channels):
-  // two ds_read_b64_tr_b16 per operand (CDNA4 hardware transpose read).
-  static constexpr int KSTEP = 32;
-  typedef bf16x8 frag;
-  __device__ static __forceinline__ frag tr_load(const bf16* row_q, const bf16* row_q4) {
-    i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(row_q));
-    i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(row_q4));
-    typedef __attribute__((ext_vector_type(8))) short i16x8;
-    i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, r);
-  }
-};
-
-template <typename T, int KS>
-__global__ __launch_bounds__(NTHR) void wgrad_kernel(const unet_wgrad_desc d, int tiles_w, int tiles_h, int mtiles,
-                                                      int per_split, float* ws) {
-  using M = Mma<T>;
-  constexpr int KC = M::KC, VEC = Vec<T>::N, NV = KC / VEC;
-  constexpr int BCI = 2 * KC;                     // 64 (bf16) / 32 (f32) input channels per block
-  constexpr int HALO = (KS == 3) ? 1 : 0;
-  constexpr int HWID = TW + 2 * HALO, HHGT = TH + 2 * HALO, HP = HWID * HHGT;
-  constexpr int RSX = BCI + 16 / (int)sizeof(T);
-  constexpr int RSD = WG_BCO + 16 / (int)sizeof(T);
-  constexpr int TAPS = KS * KS;
-  constexpr int NTN = BCI / 32;                   // n-tiles (ci) per wave
-  constexpr int KSTEP = M::KSTEP;                 // pixels per MFMA
-  __shared__ __attribute__((aligned(16))) T lds[HP * RSX + BM * RSD];
-  T* lds_x = lds;
-  T* lds_d = lds + HP * RSX;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wco = wave >> 1, wci = wave & 1;
-  const int split = blockIdx.x;
-  const int ci0 = blockIdx.y * BCI;
-  const int co0 = blockIdx.z * WG_BCO;
-
-  f32x4 acc[TAPS][2][NTN];
-#pragma unroll
-  for (int t = 0; t < TAPS; ++t)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NTN; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int mt_begin = split * per_split;
-  const int mt_end = min(mtiles, mt_begin + per_split);
-  const T* dy = (const T*)d.dy;
-  for (int mt = mt_begin; mt < mt_end; ++mt) {
-    const int tw_i = mt % tiles_w;
-    const int t2 = mt / tiles_w;
-    const int th_i = t2 % tiles_h;
-    const long long n = t2 / tiles_h;
-    const int h0 = th_i * TH, w0 = tw_i * TW;
-    // dy tile [BM][WG_BCO]
-    constexpr int DV = WG_BCO / VEC;
-    for (int it = tid; it < BM * DV; it += NTHR) {
-      const int p = it / DV, v = it % DV;
-      const int oh = h0 + p / TW, ow = w0 + p % TW;
-      const int co = co0 + v * VEC;
-      float vals[VEC];
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) vals[j] = 0.f;
-      if (oh < d.H && ow < d.W && co < d.Cout) {
-        const T* src = dy + ((n * d.H + oh) * (long long)d.W + ow) * d.Cout + co;
-        if (co + VEC <= d.Cout && (d.Cout % VEC) == 0) {
-          load_vec<T>(src, vals);
-        } else {
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) vals[j] = (co + j < d.Cout) ? to_f(src[j]) : 0.f;
-        }
-      }
-      store_vec<T>(lds_d + p * RSD + v * VEC, vals);
-    }
-    // input halo [HP][BCI]
-    for (int it = tid; it < HP * 2 * NV; it += NTHR) {
-      const int hp = it / (2 * NV), v = it % (2 * NV);
-      const int hy = h0 + hp / HWID - HALO, hx = w0 + hp % HWID - HALO;
-      float vals[VEC];
-      src_gather<T>(d.src, d.nsrc, d.Cin, d.H, d.W, n, hy, hx, ci0 + v * VEC, vals);
-      store_vec<T>(lds_x + hp * RSX + v * VEC, vals);
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int k0 = 0; k0 < BM; k0 += KSTEP) {
-      typename M::frag a[2];
-      if constexpr (sizeof(T) == 2) {
-        const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = (i16 & 3) * 4;
-        const int pr = k0 + 8 * g + q;  // pixel row of the tr-read block (and +4)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int m0 = wco * 32 + i * 16 + p4;
-          a[i] = WgFrag<bf16>::tr_load(lds_d + pr * RSD + m0, lds_d + (pr + 4) * RSD + m0);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) a[i] = M::load(lds_d + (k0 + (lane >> 4)) * RSD + wco * 32 + i * 16 + (lane & 15));
-      }
-#pragma unroll
-      for (int tap = 0; tap < TAPS; ++tap) {
-        const int dy_ = tap / KS, dx_ = tap % KS;
-        typename M::frag b[NTN];
-        if constexpr (sizeof(T) == 2) {
-          const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p4 = (i16 & 3) * 4;
-          const int p0 = k0 + 8 * g + q, p1 = p0 + 4;
-          const int hp0 = (p0 / TW + dy_) * HWID + p0 % TW + dx_;
-          const int hp1 = (p1 / TW + dy_) * HWID + p1 % TW + dx_;
-#pragma unroll
-          for (int j = 0; j < NTN; ++j) {
-            const int n0 = wci * (BCI / 2) + j * 16 + p4;
-            b[j] = WgFrag<bf16>::tr_load(lds_x + hp0 * RSX + n0, lds_x + hp1 * RSX + n0);
-          }
-        } else {
-          const int p = k0 + (lane >> 4);
-          const int hp = (p / TW + dy_) * HWID + p % TW + dx_;
-#pragma unroll
-          for (int j = 0; j < NTN; ++j) b[j] = M::load(lds_x + hp * RSX + wci * (BCI / 2) + j * 16 + (lane & 15));
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < NTN; ++j) acc[tap][i][j] = M::mma(a[i], b[j], acc[tap][i][j]);
-      }
-    }
-    __syncthreads();
-  }
-  // slab write: ws[split][co][tap][ci]  (C layout: row = co = 4*(l>>4)+r, col = ci = l&15)
-  float* slab = ws + (size_t)split * d.Cout * TAPS * d.Cin;
-#pragma unroll
-  for (int tap = 0; tap < TAPS; ++tap)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NTN; ++j) {
-        const int ci = ci0 + wci * (BCI / 2) + j * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = co0 + wco * 32 + i * 16 + 4 * (lane >> 4) + r;
-          if (co < d.Cout && ci < d.Cin) slab[((size_t)co * TAPS + tap) * d.Cin + ci] = acc[tap][i][j][r];
-        }
-      }
-}
-
-// dw[co][ci][kh][kw] (+)= sum_s ws[s][co][tap][ci]
-__global__ void wgrad_reduce_kernel(const float* ws, int splits, int Cout, int Cin, int taps, float* dw, int accum) {
-  const long long total = (long long)Cout * Cin * taps;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const int tap = e % taps;
-    const long long t = e / taps;
-    const int ci = t % Cin;
-    const int co = t / Cin;
-    const size_t src = ((size_t)co * taps + tap) * Cin + ci;
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[(size_t)k * Cout * taps * Cin + src];
-    dw[e] = accum ? dw[e] + s : s;
-  }
-}
-
-struct WgPlan {
-  int tiles_w, tiles_h, mtiles, splits, per_split, ci_tiles, co_tiles;
-  size_t ws_bytes;
-};
-
-static WgPlan wg_plan(const unet_wgrad_desc* d) {
-  WgPlan p;
-  const int kc = d->dtype == UNET_BF16 ? 32 : 16;
-  p.tiles_w = cdiv(d->W, TW);
-  p.tiles_h = cdiv(d->H, TH);
-  p.mtiles = d->N * p.tiles_w * p.tiles_h;
-  p.ci_tiles = cdiv(d->Cin, 2 * kc);
-  p.co_tiles = cdiv(d->Cout, WG_BCO);
-  const int taps = d->ksize * d->ksize;
-  const size_t slab = (size_t)d->Cout * taps * d->Cin * sizeof(float);
-  const int tiles = p.ci_tiles * p.co_tiles;
-  int want = cdiv(1024, tiles);
-  const size_t cap = (size_t)160 << 20;
-  int by_ws = (int)(cap / (slab ? slab : 1));
-  if (by_ws < 1) by_ws = 1;
-  int s = want < by_ws ? want : by_ws;
-  if (s > p.mtiles) s = p.mtiles;
-  if (s < 1) s = 1;
-  p.per_split = cdiv(p.mtiles, s);
-  p.splits = cdiv(p.mtiles, p.per_split);
-  p.ws_bytes = slab * p.splits;
-  return p;
-}
-
-template <typename T, int KS>
-static int launch_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
-  WgPlan p = wg_plan(d);
-  float* ws = (float*)d->workspace;
-  dim3 grid(p.splits, p.ci_tiles, p.co_tiles);
-  hipLaunchKernelGGL((wgrad_kernel<T, KS>), grid, dim3(NTHR), 0, st, *d, p.tiles_w, p.tiles_h, p.mtiles,
-                     p.per_split, ws);
-  int e = check_launch("wgrad");
-  if (e) return e;
-  const long long total = (long long)d->Cout * d->Cin * KS * KS;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, p.splits, d->Cout, d->Cin, KS * KS,
-                     d->dw, d->accum);
-  return check_launch("wgrad_reduce");
-}
-
-// ------------------------------------------------------------------------------------------------
-// weight packing: OIHW fp32 -> [Cout][k*k][Cin_pad] (fwd) or [Cin][k*k flipped][Cout_pad] (dgrad)
+// weight packing: OIHW fp32 -> fragment-major [Npad/16][nchunks][taps][64][16 B]
+//   transpose=0: rows = Cout, reduction = Cin (forward);
+//   transpose=1: rows = Cin, reduction = Cout, taps flipped 180 degrees (dgrad)
 // ------------------------------------------------------------------------------------------------
 template <typename T>
-__global__ void pack_kernel(const float* w, T* out, int Cout, int Cin, int ks, int transpose, int kc) {
+__global__ void pack_kernel(const float* w, T* out, int Cout, int Cin, int ks, int transpose, int rows_pad,
+                            int nchunks) {
+  constexpr int KC = Mma<T>::KC, E16 = 16 / (int)sizeof(T);
   const int taps = ks * ks;
-  const int rows = transpose ? Cin : Cout;      // output-channel axis of the packed operand
-  const int cols = transpose ? Cout : Cin;      // reduction-channel axis
-  const int cols_pad = (cols + kc - 1) / kc * kc;
-  const long long total = (long long)rows * taps * cols_pad;
+  const int rows = transpose ? Cin : Cout;
+  const int cols = transpose ? Cout : Cin;
+  const long long total = (long long)rows_pad * nchunks * KC * taps;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const int c = e % cols_pad;
-    const long long t = e / cols_pad;
+    const int el = e % E16;
+    long long t = e / E16;
+    const int lane = t % 64;
+    t /= 64;
     const int tap = t % taps;
-    const int r = t / taps;
+    t /= taps;
+    const int chunk = t % nchunks;
+    const int ntile = t / nchunks;
+    const int r = ntile * 16 + (lane & 15);
+    const int k = (sizeof(T) == 2) ? 8 * (lane >> 4) + el : 4 * el + (lane >> 4);
+    const int cc = chunk * KC + k;
     float v = 0.f;
-    if (c < cols) {
-      if (!transpose) {
-        v = w[((long long)r * Cin + c) * taps + tap];                      // w[co=r][ci=c][tap]
-      } else {
-        const int ftap = taps - 1 - tap;                                 // 180-degree flip
-        v = w[((long long)c * Cin + r) * taps + ftap];                     // w[co=c][ci=r][flip(tap)]
-      }
+    if (r < rows && cc < cols) {
+      if (!transpose) v = w[((long long)r * Cin + cc) * taps + tap];
+      else v = w[((long long)cc * Cin + r) * taps + (taps - 1 - tap)];
     }
     out[e] = from_f<T>(v);
   }
+}
+
+static int packed_rows(int Cout, int Cin, int transpose) {
+  return round_up(transpose ? Cin : Cout, PACK_NPAD);
 }
 
 }  // namespace unet
@@ -491,26 +386,47 @@ using namespace unet;
 
 extern "C" {
 
-int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, TW) * cdiv(H, TH); }
+int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8); }
+
+int unet_conv_stats_rows(const unet_conv_desc* d) {
+  if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
+  const ConvCfg c = pick_cfg(d);
+  return d->N * cdiv(d->W, CTW) * cdiv(d->H, 4 * c.wm);
+}
+
+int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
+  if (!fast_eligible(d)) {
+    snprintf(buf, len, "conv_generic_kernel<%s,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize,
+             d->Cout <= 32 ? 32 : 64);
+    return 0;
+  }
+  const ConvCfg c = pick_cfg(d);
+  snprintf(buf, len, "conv2_kernel<%s,%d,%d,%d,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize, c.wm,
+           c.wn, c.ntn, c.raw);
+  return 0;
+}
 
 int unet_packed_weight_elems(int dtype, int Cout, int Cin, int ksize, int transpose) {
   const int kc = dtype == UNET_BF16 ? 32 : 16;
-  const int rows = transpose ? Cin : Cout, cols = transpose ? Cout : Cin;
-  return rows * ksize * ksize * round_up(cols, kc);
+  const int cols = transpose ? Cout : Cin;
+  return packed_rows(Cout, Cin, transpose) * ksize * ksize * round_up(cols, kc);
 }
 
 int unet_pack_weight(int dtype, const float* w, void* packed, int Cout, int Cin, int ksize, int transpose,
                      void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const long long total = unet_packed_weight_elems(dtype, Cout, Cin, ksize, transpose);
+  const int kc = dtype == UNET_BF16 ? 32 : 16;
+  const int rows_pad = packed_rows(Cout, Cin, transpose);
+  const int nchunks = cdiv(transpose ? Cout : Cin, kc);
+  const long long total = (long long)rows_pad * nchunks * kc * ksize * ksize;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   if (dtype == UNET_BF16)
     hipLaunchKernelGGL(pack_kernel<bf16>, dim3(blocks), dim3(256), 0, st, w, (bf16*)packed, Cout, Cin, ksize,
-                       transpose, 32);
+                       transpose, rows_pad, nchunks);
   else
     hipLaunchKernelGGL(pack_kernel<float>, dim3(blocks), dim3(256), 0, st, w, (float*)packed, Cout, Cin, ksize,
-                       transpose, 16);
+                       transpose, rows_pad, nchunks);
   return check_launch("pack_weight");
 }
 
@@ -547,27 +463,6 @@ int unet_conv(const unet_conv_desc* d, void* stream) {
   if (d->dtype == UNET_BF16) return dispatch_conv<bf16>(d, st);
   if (d->dtype == UNET_F32) return dispatch_conv<float>(d, st);
   set_error("unet_conv: bad dtype");
-  return UNET_ERR_ARG;
-}
-
-size_t unet_wgrad_workspace(const unet_wgrad_desc* d) { return wg_plan(d).ws_bytes; }
-
-int unet_conv_wgrad(const unet_wgrad_desc* d, void* stream) {
-  if (!d || d->N <= 0 || d->H <= 0 || d->W <= 0 || d->Cin <= 0 || d->Cout <= 0 || !d->dy || !d->dw ||
-      !d->workspace || (d->ksize != 1 && d->ksize != 3) || d->nsrc < 1 || d->nsrc > 2) {
-    set_error("unet_conv_wgrad: bad descriptor");
-    return UNET_ERR_ARG;
-  }
-  int csum = 0;
-  for (int i = 0; i < d->nsrc; ++i) {
-    if (!validate_src(d->src[i])) { set_error("unet_conv_wgrad: bad source"); return UNET_ERR_ARG; }
-    csum += d->src[i].C;
-  }
-  if (csum != d->Cin) { set_error("unet_conv_wgrad: source channels != Cin"); return UNET_ERR_ARG; }
-  hipStream_t st = (hipStream_t)stream;
-  if (d->dtype == UNET_BF16) return d->ksize == 3 ? launch_wgrad<bf16, 3>(d, st) : launch_wgrad<bf16, 1>(d, st);
-  if (d->dtype == UNET_F32) return d->ksize == 3 ? launch_wgrad<float, 3>(d, st) : launch_wgrad<float, 1>(d, st);
-  set_error("unet_conv_wgrad: bad dtype");
   return UNET_ERR_ARG;
 }
 

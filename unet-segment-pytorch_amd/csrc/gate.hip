@@ -107,6 +107,126 @@ __global__ void gate_bwd1_kernel(long long P, int Cx, const float* dxs, const T*
   }
 }
 
+// ---- coalesced variants: a group of G = C/8 lanes owns one pixel (8 channels per lane); per-pixel
+// channel sums by xor-shuffles inside the group.  Used when C % 8 == 0 and C/8 is a power of two <= 64.
+__device__ __forceinline__ float group_sum(float v, int G) {
+  for (int o = G >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    load_vec<bf16>((const bf16*)p, v);
+  } else {
+    load_vec<float>((const float*)p, v);
+    load_vec<float>((const float*)p + 4, v + 4);
+  }
+}
+
+template <typename T>
+__global__ void psi_vec_kernel(long long P, int Ci, int G, const T* gw, const T* xw, const float* gab, const float* xab,
+                               const float* wpsi, float* p, float* part, int rows) {
+  __shared__ float sh[8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int sub = lane % G, ppw = 64 / G;
+  const int c0 = sub * 8;
+  float gs[8], gb[8], xs[8], xb[8], w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    gs[j] = gab[c0 + j]; gb[j] = gab[Ci + c0 + j]; xs[j] = xab[c0 + j]; xb[j] = xab[Ci + c0 + j]; w[j] = wpsi[c0 + j];
+  }
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  float s = 0.f, ss = 0.f;
+  for (long long q = p0 + wave * ppw + lane / G; q < p1; q += (long long)nw * ppw) {
+    float g[8], x[8];
+    load8<T>(gw + q * Ci + c0, g);
+    load8<T>(xw + q * Ci + c0, x);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += w[j] * fmaxf(g[j] * gs[j] + gb[j] + x[j] * xs[j] + xb[j], 0.f);
+    acc = group_sum(acc, G);
+    if (sub == 0) {
+      p[q] = acc;
+      s += acc;
+      ss += acc * acc;
+    }
+  }
+  s = block_sum_f(s, sh);
+  ss = block_sum_f(ss, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s;
+    part[rows + blockIdx.x] = ss;
+  }
+}
+
+template <typename T>
+__global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* dxs, const T* yx, const float* sx,
+                                     const float* bx, int relu, const float* pp, const float* psi_ab,
+                                     const float* psi_mean, const float* psi_inv, float* dx, int dx_accum, float* dq,
+                                     float* part, int rows) {
+  __shared__ float sh[8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int sub = lane % G, ppw = 64 / G;
+  const int c0 = sub * 8;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = sx[c0 + j]; sf[j] = bx[c0 + j]; }
+  const float pa = psi_ab[0], pb = psi_ab[1], pm = psi_mean[0], pi = psi_inv[0];
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  float s1 = 0.f, s2 = 0.f;
+  for (long long q = p0 + wave * ppw + lane / G; q < p1; q += (long long)nw * ppw) {
+    float d[8], y[8];
+    load_vec<float>(dxs + q * Cx + c0, d);
+    load_vec<float>(dxs + q * Cx + c0 + 4, d + 4);
+    load8<T>(yx + q * Cx + c0, y);
+    const float pv = pp[q];
+    const float sg = sigmoidf_(pv * pa + pb);
+    float ds = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float xv = y[j] * sc[j] + sf[j];
+      if (relu) xv = fmaxf(xv, 0.f);
+      ds += d[j] * xv;
+    }
+    float* o = dx + q * Cx + c0;
+    float g[8];
+    if (dx_accum) {
+      load_vec<float>(o, g);
+      load_vec<float>(o + 4, g + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] += d[j] * sg;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = d[j] * sg;
+    }
+    store_vec<float>(o, g);
+    store_vec<float>(o + 4, g + 4);
+    ds = group_sum(ds, G);
+    if (sub == 0) {
+      const float dqv = ds * sg * (1.f - sg);
+      dq[q] = dqv;
+      s1 += dqv;
+      s2 += dqv * (pv - pm) * pi;
+    }
+  }
+  s1 = block_sum_f(s1, sh);
+  s2 = block_sum_f(s2, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s1;
+    part[rows + blockIdx.x] = s2;
+  }
+}
+
+static inline int vec_group(int C) {
+  if (C % 8) return 0;
+  const int g = C / 8;
+  if (g > 64 || (g & (g - 1))) return 0;
+  return g;
+}
+
 // channel lanes x pixel rows
 template <typename T>
 __global__ void gate_bwd2_kernel(long long P, int Ci, int CL, const T* gw, const T* xw, const float* gab,
@@ -185,6 +305,16 @@ int unet_gate_psi_rows(long long P) { return pix_rows(P); }
 int unet_gate_psi(int dtype, long long P, int Ci, const void* gw, const void* xw, const float* gab, const float* xab,
                   const float* wpsi, float* p, float* partial, void* stream) {
   const int rows = pix_rows(P);
+  const int G = vec_group(Ci);
+  if (G) {
+    if (dtype == UNET_BF16)
+      hipLaunchKernelGGL(psi_vec_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, G,
+                         (const bf16*)gw, (const bf16*)xw, gab, xab, wpsi, p, partial, rows);
+    else
+      hipLaunchKernelGGL(psi_vec_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, G,
+                         (const float*)gw, (const float*)xw, gab, xab, wpsi, p, partial, rows);
+    return check_launch("gate_psi");
+  }
   if (dtype == UNET_BF16)
     hipLaunchKernelGGL(psi_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, (const bf16*)gw,
                        (const bf16*)xw, gab, xab, wpsi, p, partial, rows);
@@ -198,6 +328,18 @@ int unet_gate_bwd1(int dtype, long long P, int Cx, const float* dxs, const void*
                    int relu, const float* p, const float* psi_ab, const float* psi_mean, const float* psi_invstd, float* dx,
                    int dx_accum, float* dq, float* partial, void* stream) {
   const int rows = pix_rows(P);
+  const int G = vec_group(Cx);
+  if (G) {
+    if (dtype == UNET_BF16)
+      hipLaunchKernelGGL(gate_bwd1_vec_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, G, dxs,
+                         (const bf16*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial,
+                         rows);
+    else
+      hipLaunchKernelGGL(gate_bwd1_vec_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, G, dxs,
+                         (const float*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial,
+                         rows);
+    return check_launch("gate_bwd1");
+  }
   if (dtype == UNET_BF16)
     hipLaunchKernelGGL(gate_bwd1_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, dxs,
                        (const bf16*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial, rows);

@@ -137,6 +137,51 @@ __global__ void outconv_fwd_kernel(long long P, int HW, int C, int K, const T* y
   }
 }
 
+// coalesced variant: G = C/8 lanes per pixel, 8 channels per lane, class sums by xor-shuffles
+template <typename T, int KT>
+__global__ void outconv_fwd_vec_kernel(long long P, int HW, int C, int G, const T* y, const float* sc, const float* sf,
+                                       int relu, const float* w, const float* b, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int sub = lane % G, ppw = 64 / G;
+  const int c0 = sub * 8;
+  float s[8], f[8], wk[KT][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s[j] = sc ? sc[c0 + j] : 1.f;
+    f[j] = sf ? sf[c0 + j] : 0.f;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) wk[k][j] = w[k * C + c0 + j];
+  }
+  const long long stride = (long long)gridDim.x * nw * ppw;
+  for (long long q = ((long long)blockIdx.x * nw + wave) * ppw + lane / G; q < P; q += stride) {
+    float a[8];
+    if constexpr (sizeof(T) == 2) {
+      load_vec<bf16>((const bf16*)y + q * C + c0, a);
+    } else {
+      load_vec<float>((const float*)y + q * C + c0, a);
+      load_vec<float>((const float*)y + q * C + c0 + 4, a + 4);
+    }
+    float acc[KT];
+#pragma unroll
+    for (int k = 0; k < KT; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = a[j] * s[j] + f[j];
+      if (relu) v = fmaxf(v, 0.f);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) acc[k] += wk[k][j] * v;
+    }
+#pragma unroll
+    for (int k = 0; k < KT; ++k)
+      for (int o = G >> 1; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+    if (sub == 0) {
+      const long long n = q / HW, hw = q % HW;
+#pragma unroll
+      for (int k = 0; k < KT; ++k) out[(n * KT + k) * HW + hw] = acc[k] + b[k];
+    }
+  }
+}
+
 // channel lanes x pixel rows: da[p][c] (+)= Σ_k w[k][c] dl[k][p]; partial dW[k][c], db[k]
 template <typename T>
 __global__ void outconv_bwd_kernel(long long P, int HW, int C, int CL, int K, const T* y, const float* sc,
@@ -320,6 +365,18 @@ int unet_outconv_fwd(int dtype, long long N, int H, int W, int C, int K, const v
                      const float* shift, int relu, const float* w, const float* b, float* logits, void* stream) {
   if (K > OC_MAXK || K < 1) { set_error("unet_outconv_fwd: n_classes > 8 unsupported"); return UNET_ERR_UNSUPPORTED; }
   const long long P = N * H * (long long)W;
+  const int G = (C % 8 == 0 && C / 8 <= 64 && ((C / 8) & (C / 8 - 1)) == 0) ? C / 8 : 0;
+  if (G && K == 2) {
+    long long blocks = (P * G + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (dtype == UNET_BF16)
+      hipLaunchKernelGGL((outconv_fwd_vec_kernel<bf16, 2>), dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, P,
+                         H * W, C, G, (const bf16*)y, scale, shift, relu, w, b, logits);
+    else
+      hipLaunchKernelGGL((outconv_fwd_vec_kernel<float, 2>), dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, P,
+                         H * W, C, G, (const float*)y, scale, shift, relu, w, b, logits);
+    return check_launch("outconv_fwd");
+  }
   const size_t shm = (size_t)(K * C + 2 * C) * sizeof(float);
   if (dtype == UNET_BF16)
     hipLaunchKernelGGL(outconv_fwd_kernel<bf16>, dim3(grid_for(P)), dim3(256), shm, (hipStream_t)stream, P, H * W, C, K,

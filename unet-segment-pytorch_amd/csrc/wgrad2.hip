@@ -1,0 +1,290 @@
+// wgrad2.hip — pipelined bf16 weight gradient on MFMA (gfx950).
+//
+// dW[co][ci][tap] = Σ_pix dy[pix][co] · X[pix + off(tap)][ci]   (weight half of convolution_backward of
+// nn.Conv2d, unet/models/layers.py:32,35,152,158; X = the conv input re-gathered through its unet_src
+// descriptors exactly as the forward saw it).
+//
+// GEMM view: M = co, N = (tap, ci), K = pixels.  One workgroup = 4 waves (one per SIMD, up to 512
+// VGPRs each) owns a BCO x BCI x 9 output block and walks a range of 8x16-pixel tiles (split-K):
+//  * the dy tile [128 px][BCO] and the input halo [(8+2) x 18][BCI] are double-buffered in LDS; the
+//    next tile's raw loads are issued before this tile's MFMAs and transformed/stored after them;
+//  * each wave holds 64 co x 16 ci x 9 taps of fp32 accumulators (36 MFMA tiles); per 32-pixel K step
+//    it reads 4 dy fragments (re-used by all 9 taps) and 9 halo fragments, all with the CDNA4
+//    transposed LDS read ds_read_b64_tr_b16 (K runs along LDS rows);
+//  * partial sums go to an fp32 slab per split in OIHW order; wgrad_reduce2 sums the slabs in a fixed
+//    order (deterministic) with 16-byte accesses.
+#include "halo_items.h"
+
+namespace unet {
+
+constexpr int W2_TH = 8, W2_TW = 16, W2_BM = 128, W2_NT = 256;
+
+__device__ __forceinline__ bf16x8 tr8(const bf16* r0, const bf16* r1) {
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r0));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r1));
+  typedef __attribute__((ext_vector_type(8))) short i16x8;
+  const i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int KS, int WCO, int WCI, int RAW>
+__global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, int tiles_w, int tiles_h, int mtiles,
+                                                      int per_split, float* ws) {
+  using T = bf16;
+  constexpr int VEC = 8;
+  constexpr int BCO = WCO * 64, BCI = WCI * 16;
+  constexpr int HALO = (KS == 3) ? 1 : 0;
+  constexpr int HWID = W2_TW + 2 * HALO, HHGT = W2_TH + 2 * HALO, HP = HWID * HHGT;
+  constexpr int RSX = BCI + 8, RSD = BCO + 8;  // LDS rows padded by 16 B
+  constexpr int TAPS = KS * KS;
+  constexpr int NVX = BCI / VEC, NVD = BCO / VEC;
+  constexpr int IX = (HP * NVX + W2_NT - 1) / W2_NT;
+  constexpr int ID = (W2_BM * NVD + W2_NT - 1) / W2_NT;
+  constexpr int BUF = HP * RSX + W2_BM * RSD;
+  static_assert(W2_NT % NVX == 0 && W2_NT % NVD == 0, "fixed channel vector per thread");
+  __shared__ __attribute__((aligned(16))) T lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave / WCI, wci = wave % WCI;
+  const int split = blockIdx.x;
+  const int ci0 = blockIdx.y * BCI;
+  const int co0 = blockIdx.z * BCO;
+  const int mt_begin = split * per_split;
+  const int mt_end = min(mtiles, mt_begin + per_split);
+
+  // fixed per-thread channel vectors
+  const int vx = tid % NVX, vd = tid % NVD;
+  SrcView sv;
+  float sc[VEC], sf[VEC];
+  make_view<T>(d, ci0 + vx * VEC, sv, sc, sf);
+  const int cod = co0 + vd * VEC;
+  const bool dy_ok = cod < d.Cout;
+  const char* dyb = (const char*)d.dy;
+
+  auto tile_nhw = [&](int mt, long long& n, int& h0, int& w0) {
+    const int tw_i = mt % tiles_w;
+    const int t2 = mt / tiles_w;
+    h0 = (t2 % tiles_h) * W2_TH;
+    w0 = tw_i * W2_TW;
+    n = t2 / tiles_h;
+  };
+
+  // staging of a tile, split into pieces so that only a few raw loads are in flight at once:
+  //   dy vectors: issued at K-step 0, stored after K-step 1; halo item k: issued at K-step
+  //   (3k / IX), stored after the following K-step (see the main loop)
+  Item<RAW> xi[IX];
+  uint4 dq[ID];
+  auto issue_x = [&](int mt, int k) {
+    long long n;
+    int h0, w0;
+    tile_nhw(mt, n, h0, w0);
+    const int hp = (tid + k * W2_NT) / NVX;
+    item_issue<T, RAW>(sv, d.H, d.W, n, h0 + hp / HWID - HALO, w0 + hp % HWID - HALO, hp < HP, xi[k]);
+  };
+  auto finish_x = [&](int mt, int k, T* buf) {
+    long long n;
+    int h0, w0;
+    tile_nhw(mt, n, h0, w0);
+    const int hp = (tid + k * W2_NT) / NVX;
+    if (hp < HP) {
+      float vals[VEC];
+      item_finish<T, RAW>(d, sv, sc, sf, n, h0 + hp / HWID - HALO, w0 + hp % HWID - HALO, ci0 + vx * VEC, xi[k], vals);
+      store_vec<T>(buf + hp * RSX + vx * VEC, vals);
+    }
+  };
+  auto issue_d = [&](int mt) {
+    long long n;
+    int h0, w0;
+    tile_nhw(mt, n, h0, w0);
+#pragma unroll
+    for (int k = 0; k < ID; ++k) {
+      const int p = (tid + k * W2_NT) / NVD;
+      const int oh = h0 + p / W2_TW, ow = w0 + p % W2_TW;
+      dq[k] = make_uint4(0, 0, 0, 0);
+      if (dy_ok && p < W2_BM && oh < d.H && ow < d.W)
+        dq[k] = ld16<T>(dyb, ((n * d.H + oh) * (long long)d.W + ow) * d.Cout + cod);
+    }
+  };
+  auto finish_d = [&](T* buf) {
+    T* bd = buf + HP * RSX;
+#pragma unroll
+    for (int k = 0; k < ID; ++k) {
+      const int p = (tid + k * W2_NT) / NVD;
+      if (p < W2_BM) *reinterpret_cast<uint4*>(bd + p * RSD + vd * VEC) = dq[k];
+    }
+  };
+  auto issue = [&](int mt) {
+#pragma unroll
+    for (int k = 0; k < IX; ++k) issue_x(mt, k);
+    issue_d(mt);
+  };
+  auto finish = [&](int mt, T* buf) {
+#pragma unroll
+    for (int k = 0; k < IX; ++k) finish_x(mt, k, buf);
+    finish_d(buf);
+  };
+
+  f32x4 acc[TAPS][4];
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (mt_begin < mt_end) {
+    issue(mt_begin);
+    finish(mt_begin, lds);
+  }
+  __syncthreads();
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+  for (int mt = mt_begin; mt < mt_end; ++mt) {
+    const int cur = (mt - mt_begin) & 1;
+    const T* bx = lds + cur * BUF;
+    const T* bd = bx + HP * RSX;
+    const bool has_next = mt + 1 < mt_end;
+    T* nb = lds + (cur ^ 1) * BUF;
+#pragma unroll
+    for (int k0 = 0; k0 < W2_BM; k0 += 32) {
+      const int s = k0 / 32;  // K step 0..3
+      if (has_next) {
+        if (s == 0) issue_d(mt + 1);
+#pragma unroll
+        for (int k = 0; k < IX; ++k)
+          if ((3 * k) / IX == s) issue_x(mt + 1, k);
+      }
+      // lane bases + compile-time offsets (so every LDS read is base + immediate): this lane addresses
+      // pixel rows pa = k0 + 8g + q and pa + 4; pixel pa sits at tile row 2s + (g>>1), column 8(g&1) + q
+      const T* dl = bd + (8 * g + q) * RSD + wco * 64 + p4;
+      const T* xl = bx + ((g >> 1) * HWID + 8 * (g & 1) + q) * RSX + wci * 16 + p4;
+      bf16x8 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = tr8(dl + k0 * RSD + i * 16, dl + (k0 + 4) * RSD + i * 16);
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) {
+        const int dy = t / KS, dx = t % KS;
+        const int off = ((2 * s + dy) * HWID + dx) * RSX;
+        const bf16x8 b = tr8(xl + off, xl + off + 4 * RSX);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[t][i], 0, 0, 0);
+      }
+      if (has_next) {
+        if (s == 1) finish_d(nb);
+#pragma unroll
+        for (int k = 0; k < IX; ++k)
+          if ((3 * k) / IX + 1 == s) finish_x(mt + 1, k, nb);
+      }
+    }
+    __syncthreads();
+  }
+
+  // slab (OIHW order): ws[split][co][ci][tap]; C layout: row (co) = 4*(l>>4)+r, col (ci) = l&15
+  float* slab = ws + (size_t)split * d.Cout * d.Cin * TAPS;
+  const int ci = ci0 + wci * 16 + (lane & 15);
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wco * 64 + i * 16 + 4 * (lane >> 4) + r;
+        if (co < d.Cout && ci < d.Cin) slab[((size_t)co * d.Cin + ci) * TAPS + t] = acc[t][i][r];
+      }
+}
+
+// dw (+)= Σ_s ws[s]   (fixed order; 16-byte accesses when the size allows)
+__global__ void wgrad_reduce2_kernel(const float* ws, int splits, long long total, float* dw, int accum) {
+  if ((total & 3) == 0) {
+    const long long n4 = total / 4;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n4; e += (long long)gridDim.x * blockDim.x) {
+      float4 s = reinterpret_cast<const float4*>(ws)[e];
+      for (int k = 1; k < splits; ++k) {
+        const float4 v = reinterpret_cast<const float4*>(ws + (size_t)k * total)[e];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      float4* o = reinterpret_cast<float4*>(dw) + e;
+      if (accum) {
+        const float4 a = *o;
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+      }
+      *o = s;
+    }
+  } else {
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+      float s = ws[e];
+      for (int k = 1; k < splits; ++k) s += ws[(size_t)k * total + e];
+      dw[e] = accum ? dw[e] + s : s;
+    }
+  }
+}
+
+struct W2Plan {
+  bool ok;
+  int wco, wci, raw, tiles_w, tiles_h, mtiles, splits, per_split;
+  size_t ws_bytes;
+};
+
+W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
+  W2Plan p{};
+  p.ok = d->dtype == UNET_BF16 && (d->Cout % 8) == 0;
+  p.raw = 1;
+  for (int i = 0; i < d->nsrc; ++i) {
+    const unet_src& s = d->src[i];
+    if (s.kind == UNET_SRC_NCHW_F32 || (s.C % 8)) p.ok = false;
+    if (s.kind == UNET_SRC_POOL_ACT || s.kind == UNET_SRC_UP_ACT) p.raw = 4;
+  }
+  if (!p.ok) return p;
+  if (d->Cout <= 64) { p.wco = 1; p.wci = 4; } else { p.wco = 2; p.wci = 2; }
+  const int bco = p.wco * 64, bci = p.wci * 16;
+  p.tiles_w = cdiv(d->W, W2_TW);
+  p.tiles_h = cdiv(d->H, W2_TH);
+  p.mtiles = d->N * p.tiles_w * p.tiles_h;
+  const long long tiles_out = (long long)cdiv(d->Cout, bco) * cdiv(d->Cin, bci);
+  const size_t slab = (size_t)d->Cout * d->Cin * d->ksize * d->ksize * sizeof(float);
+  long long s = (512 + tiles_out - 1) / tiles_out;
+  const long long cap = (long long)(((size_t)96 << 20) / (slab ? slab : 1));
+  if (s > cap) s = cap;
+  if (s > p.mtiles) s = p.mtiles;
+  if (s < 1) s = 1;
+  p.per_split = cdiv(p.mtiles, s);
+  p.splits = cdiv(p.mtiles, p.per_split);
+  p.ws_bytes = slab * p.splits;
+  return p;
+}
+
+template <int KS, int WCO, int WCI, int RAW>
+static int launch_w2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
+  dim3 grid(p.splits, cdiv(d->Cin, WCI * 16), cdiv(d->Cout, WCO * 64));
+  hipLaunchKernelGGL((wgrad2_kernel<KS, WCO, WCI, RAW>), grid, dim3(W2_NT), 0, st, *d, p.tiles_w, p.tiles_h, p.mtiles,
+                     p.per_split, (float*)d->workspace);
+  return check_launch("wgrad2");
+}
+
+template <int KS, int RAW>
+static int launch_w2_cfg(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
+  if (p.wco == 1) return launch_w2<KS, 1, 4, RAW>(d, p, st);
+  return launch_w2<KS, 2, 2, RAW>(d, p, st);
+}
+
+int launch_wgrad2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
+  int e;
+  if (d->ksize == 3) e = p.raw == 4 ? launch_w2_cfg<3, 4>(d, p, st) : launch_w2_cfg<3, 1>(d, p, st);
+  else e = p.raw == 4 ? launch_w2_cfg<1, 4>(d, p, st) : launch_w2_cfg<1, 1>(d, p, st);
+  if (e) return e;
+  const long long total = (long long)d->Cout * d->Cin * d->ksize * d->ksize;
+  long long blocks = (total / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(wgrad_reduce2_kernel, dim3((int)blocks), dim3(256), 0, st, (const float*)d->workspace, p.splits,
+                     total, d->dw, d->accum);
+  return check_launch("wgrad_reduce2");
+}
+
+// entry points used by wgrad.hip (which keeps the generic kernel for fp32 / odd channel counts)
+bool wgrad2_eligible(const unet_wgrad_desc* d, size_t* ws_bytes) {
+  const W2Plan p = wgrad2_plan(d);
+  if (p.ok && ws_bytes) *ws_bytes = p.ws_bytes;
+  return p.ok;
+}
+int wgrad2_run(const unet_wgrad_desc* d, hipStream_t st) { return launch_wgrad2(d, wgrad2_plan(d), st); }
+
+}  // namespace unet

@@ -66,8 +66,8 @@ class KernelProbe:
     def reset(self):
         self.records = []
 
-    def launch(self, name: str, flops: float, fn):
-        if self.target is None or name != self.target:
+    def launch(self, name_fn, flops: float, fn):
+        if self.target is None or not name_fn().startswith(self.target):
             return fn()
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
@@ -89,10 +89,11 @@ class KernelProbe:
 probe = KernelProbe()
 
 
-def conv_kernel_name(prec: "Precision", ksize: int, cout: int) -> str:
-    """Symbol family chosen by unet_conv's dispatch (csrc/conv.hip dispatch_conv)."""
-    bn = 32 if cout <= 32 else 64
-    return f"conv_kernel<{prec.name},{ksize},{bn}>"
+def conv_kernel_name(d) -> str:
+    """Instantiation unet_conv dispatches this descriptor to (csrc/conv.hip dispatch_conv)."""
+    buf = ctypes.create_string_buffer(128)
+    L.load().unet_conv_variant(d, buf, 128)
+    return buf.value.decode()
 
 
 def wgrad_kernel_name(prec: "Precision", ksize: int) -> str:

@@ -70,10 +70,10 @@ class ConvBN:
         ab = f32(2, self.cout, device=dev)
         use_batch = training or not bn.track_running_stats
         if use_batch:
-            mt = L.load().unet_conv_mtiles(N, H, W)
+            mt = L.load().unet_conv_stats_rows(d)
             stats = f32(2, mt, self.cout, device=dev)
             d.stats = stats.data_ptr()
-        probe.launch(conv_kernel_name(prec, self.k, self.cout), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
+        probe.launch(lambda: conv_kernel_name(d), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
                      lambda: L.call("unet_conv", d, stream()))
         mean = invstd = None
         if use_batch:
@@ -132,7 +132,7 @@ class ConvBN:
         ws_bytes = L.load().unet_wgrad_workspace(wd)
         ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
         wd.workspace = ws.data_ptr()
-        probe.launch(wgrad_kernel_name(prec, self.k), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
+        probe.launch(lambda: wgrad_kernel_name(prec, self.k), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
                      lambda: L.call("unet_conv_wgrad", wd, stream()))
         grads.put(self.conv.weight, dw)
         if dgrad is None:
@@ -151,7 +151,7 @@ class ConvBN:
             o2 = dgrad.get("out2")
             d.out2 = o2.data_ptr() if o2 is not None else None
             d.accum2 = int(dgrad.get("accum2", 0))
-        probe.launch(conv_kernel_name(prec, self.k, self.cin), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
+        probe.launch(lambda: conv_kernel_name(d), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
                      lambda: L.call("unet_conv", d, stream()))
 
 
