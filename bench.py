@@ -169,7 +169,7 @@ def main():
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                      "launches": ps["launches"], "avg_us": round(ps["avg_us"], 2) if ps["avg_us"] else None,
                      "flops_per_launch": round(ps["flops"] / ps["launches"]) if ps["launches"] else None},
-        "final_loss": round(float(loss), 5),
+        "final_loss": round(float(loss.detach()), 5),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.model, args.size, args.cpu_batch, args.cpu_iters)

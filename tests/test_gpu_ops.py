@@ -200,3 +200,49 @@ def test_conv_wgrad(prec, shape, k, kind):
     torch.cuda.synchronize()
     tol = 1e-3 if prec == "bf16" else 1e-4
     assert (dw - ref).abs().max() <= tol * (1 + ref.abs().max()), float((dw - ref).abs().max())
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("shape", [(2, 1, 40, 36, 64), (1, 3, 33, 50, 16), (4, 1, 64, 64, 8)])
+def test_first_conv_nchw_input(prec, shape):
+    """inc.0: the fp32 NCHW model input read directly (csrc/smallcin.hip), fwd + BN sums + wgrad."""
+    L, R = _lib(), _rt()
+    P = R.BF16 if prec == "bf16" else R.FP32
+    N, cin, H, W, cout = shape
+    dt = DT[prec]
+    torch.manual_seed(4)
+    x = torch.rand(N, cin, H, W, device="cuda") * 2 - 1
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * 0.3).to(dt).float()
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_NCHW_F32, cin, H, W, x.data_ptr()
+    out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
+    d = L.ConvDesc()
+    d.dtype, d.N, d.H, d.W, d.Cin, d.Cout, d.ksize, d.nsrc = P.code, N, H, W, cin, cout, 3, 1
+    d.src[0] = src
+    rows = L.load().unet_conv_stats_rows(d)
+    st = torch.empty(2, rows, cout, device="cuda")
+    wp = R.pack_weight(w, P, transpose=False)
+    d.weight, d.out_mode, d.out, d.stats = wp.data_ptr(), L.OUT_Y, out.data_ptr(), st.data_ptr()
+    L.call("unet_conv", d, R.stream())
+    torch.cuda.synchronize()
+    xr = x.to(dt).float() if prec == "bf16" else x
+    ref = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)
+    tol = 1e-2 if prec == "bf16" else 1e-5
+    assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max())
+    assert torch.allclose(st[0].sum(0), ref.sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(st[1].sum(0), (ref * ref).sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
+    # weight gradient
+    dy = _rand(N, H, W, cout, dt=dt)
+    refw = torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), dy.float().permute(0, 3, 1, 2), padding=1)
+    wd = L.WgradDesc()
+    wd.dtype, wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = P.code, N, H, W, cin, cout, 3, 1
+    wd.src[0] = src
+    wd.dy = dy.data_ptr()
+    dw = torch.empty(cout, cin, 3, 3, device="cuda")
+    wd.dw = dw.data_ptr()
+    ws = torch.empty(max(L.load().unet_wgrad_workspace(wd), 16), dtype=torch.uint8, device="cuda")
+    wd.workspace = ws.data_ptr()
+    L.call("unet_conv_wgrad", wd, R.stream())
+    torch.cuda.synchronize()
+    assert (dw - refw).abs().max() <= 1e-4 * (1 + refw.abs().max())
+    del xr

@@ -32,7 +32,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_des
   constexpr int TH = 4 * WM, BN = WN * NTN * 16;
   constexpr int HALO = (KS == 3) ? 1 : 0;
   constexpr int HWID = CTW + 2 * HALO, HHGT = TH + 2 * HALO, HP = HWID * HHGT;
-  constexpr int RS = KC + 16 / (int)sizeof(T);  // 80-byte LDS rows
+  // 96-byte LDS rows (24 dwords): the 16 lanes of a ds_read_b128 phase (4 rows x 4 k-groups) hit
+  // distinct bank quads for any row base, so the A reads are conflict-free
+  constexpr int RS = KC + 32 / (int)sizeof(T);
   constexpr int TAPS = KS * KS;
   constexpr int ITEMS = (HP * NV + NT - 1) / NT;
   constexpr int E16 = 16 / (int)sizeof(T);
@@ -57,10 +59,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_des
   auto item_x = [&](int k) { return w0 + item_hp(k) % HWID - HALO; };
 
   // weight fragments: [ntile][chunk][tap][lane][16B]
-  const uint4* wbase = reinterpret_cast<const uint4*>(d.weight);
+  // (uniform byte base of this wave's first n-tile) + (uniform 32-bit offset) + lane * 16
   const int ntile0 = co0 / 16 + wn * NTN;
+  const char* wsb = reinterpret_cast<const char*>(d.weight) + (size_t)ntile0 * nchunks * TAPS * 1024;
+  const unsigned jstride = (unsigned)nchunks * TAPS * 1024u;
+  const unsigned lane16 = (unsigned)lane * 16u;
   auto bptr = [&](int j, int c, int t) -> const uint4* {
-    return wbase + ((((size_t)(ntile0 + j) * nchunks + c) * TAPS + t) * 64 + lane);
+    return reinterpret_cast<const uint4*>(wsb + (j * jstride + (unsigned)(c * TAPS + t) * 1024u + lane16));
   };
 
   f32x4 acc[4][NTN];
@@ -325,12 +330,20 @@ static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t s
 }
 
 template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
+bool smallcin_conv_ok(const unet_conv_desc* d);  // smallcin.hip
+int smallcin_rows(long long P);
+int smallcin_conv(const unet_conv_desc* d, hipStream_t st);
 
-// the pipelined kernel needs every source channel vector to be one aligned 16-byte load
+// the pipelined kernel needs every source channel vector to be one aligned 16-byte load, and every
+// source tensor addressable with 32-bit byte offsets
 static bool fast_eligible(const unet_conv_desc* d) {
   const int vec = d->dtype == UNET_BF16 ? 8 : 4;
-  for (int i = 0; i < d->nsrc; ++i)
-    if (d->src[i].kind == UNET_SRC_NCHW_F32 || d->src[i].C % vec) return false;
+  const int es = d->dtype == UNET_BF16 ? 2 : 4;
+  for (int i = 0; i < d->nsrc; ++i) {
+    const unet_src& s = d->src[i];
+    if (s.kind == UNET_SRC_NCHW_F32 || s.C % vec) return false;
+    if ((double)d->N * s.H * s.W * s.C * es >= 4294967296.0) return false;
+  }
   return true;
 }
 
@@ -389,12 +402,17 @@ extern "C" {
 int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8); }
 
 int unet_conv_stats_rows(const unet_conv_desc* d) {
+  if (smallcin_conv_ok(d)) return smallcin_rows((long long)d->N * d->H * d->W);
   if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
   const ConvCfg c = pick_cfg(d);
   return d->N * cdiv(d->W, CTW) * cdiv(d->H, 4 * c.wm);
 }
 
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
+  if (smallcin_conv_ok(d)) {
+    snprintf(buf, len, "smallcin_fwd_kernel<%s>", d->dtype == UNET_BF16 ? "bf16" : "fp32");
+    return 0;
+  }
   if (!fast_eligible(d)) {
     snprintf(buf, len, "conv_generic_kernel<%s,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize,
              d->Cout <= 32 ? 32 : 64);
@@ -460,6 +478,7 @@ int unet_conv(const unet_conv_desc* d, void* stream) {
     return UNET_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
+  if (smallcin_conv_ok(d)) return smallcin_conv(d, st);
   if (d->dtype == UNET_BF16) return dispatch_conv<bf16>(d, st);
   if (d->dtype == UNET_F32) return dispatch_conv<float>(d, st);
   set_error("unet_conv: bad dtype");

@@ -23,6 +23,45 @@ __device__ __forceinline__ float up_weight(float scale, int u, int in_size, int 
   return (i0 == i ? 1.f - l : 0.f) + (i1 == i ? l : 0.f);
 }
 
+// 4-channel vectorised form (C % 4 == 0): the index/weight arithmetic is shared by 4 channels
+__global__ void upsample_bwd4_kernel(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pt, int pl, int Hp,
+                                     int Wp, float sh, float sw, const float* dup, float* dx, int accum) {
+  const int C4 = C / 4;
+  const long long total = N * Hs * (long long)Ws * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int c4 = e % C4;
+    long long t = e / C4;
+    const int j = t % Ws;
+    t /= Ws;
+    const int i = t % Hs;
+    const long long n = t / Hs;
+    int ulo, uhi, vlo, vhi;
+    up_range(sh, i, Hs, up_h, ulo, uhi);
+    up_range(sw, j, Ws, up_w, vlo, vhi);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = ulo; u <= uhi; ++u) {
+      const float wy = up_weight(sh, u, Hs, i);
+      const int yy = u + pt;
+      if (wy == 0.f || yy < 0 || yy >= Hp) continue;
+      const float4* row = reinterpret_cast<const float4*>(dup + ((n * Hp + yy) * (long long)Wp) * C) + c4;
+      for (int v = vlo; v <= vhi; ++v) {
+        const float wx = up_weight(sw, v, Ws, j);
+        const int xx = v + pl;
+        if (wx == 0.f || xx < 0 || xx >= Wp) continue;
+        const float4 g = row[(long long)xx * C4];
+        const float w = wy * wx;
+        acc.x += w * g.x; acc.y += w * g.y; acc.z += w * g.z; acc.w += w * g.w;
+      }
+    }
+    float4* o = reinterpret_cast<float4*>(dx) + e;
+    if (accum) {
+      const float4 a = *o;
+      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    *o = acc;
+  }
+}
+
 // NHWC gather adjoint: dx[n,i,j,c] (+)= Σ_{u,v} wy(u,i) wx(v,j) d_up[n, u+pt, v+pl, c]
 __global__ void upsample_bwd_kernel(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pt, int pl, int Hp,
                                     int Wp, float sh, float sw, const float* dup, float* dx, int accum) {
@@ -250,19 +289,23 @@ __global__ void outconv_bwd_kernel(long long P, int HW, int C, int CL, int K, co
   }
 }
 
+// one block per output element; fixed-order fp64 block reduction over the partial rows
 __global__ void outconv_bwd_finalize_kernel(const float* part, int rows, int C, int K, float* dw, float* db, int accum) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int total = K * C + K;
-  if (e >= total) return;
+  __shared__ double sh[4];
+  const int e = blockIdx.x;
+  const bool is_w = e < K * C;
+  const int k = is_w ? e / C : K;
+  const int c = is_w ? e % C : e - K * C;
   double s = 0;
-  if (e < K * C) {
-    const int k = e / C, c = e % C;
-    for (int r = 0; r < rows; ++r) s += part[((size_t)r * (K + 1) + k) * C + c];
-    dw[e] = accum ? dw[e] + (float)s : (float)s;
-  } else {
-    const int k = e - K * C;
-    for (int r = 0; r < rows; ++r) s += part[((size_t)r * (K + 1) + K) * C + k];
-    db[k] = accum ? db[k] + (float)s : (float)s;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) s += part[((size_t)r * (K + 1) + k) * C + c];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float v = (float)(sh[0] + sh[1] + sh[2] + sh[3]);
+    float* o = is_w ? dw + e : db + c;
+    *o = accum ? *o + v : v;
   }
 }
 
@@ -340,6 +383,11 @@ extern "C" {
 int unet_upsample_bwd(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pad_t, int pad_l, int Hp, int Wp,
                       float sh, float sw, const float* d_up, float* dx, int accum, void* stream) {
   const long long total = N * Hs * (long long)Ws * C;
+  if (C % 4 == 0) {
+    hipLaunchKernelGGL(upsample_bwd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream, N, C, Hs,
+                       Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
+    return check_launch("upsample_bwd");
+  }
   hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, Hs, Ws,
                      up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
   return check_launch("upsample_bwd");
@@ -406,8 +454,8 @@ int unet_outconv_bwd(int dtype, long long N, int H, int W, int C, int K, const v
 int unet_outconv_bwd_finalize(const float* partial, int rows, int C, int K, float* dw, float* db, int accum,
                               void* stream) {
   const int total = K * C + K;
-  hipLaunchKernelGGL(outconv_bwd_finalize_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, partial,
-                     rows, C, K, dw, db, accum);
+  hipLaunchKernelGGL(outconv_bwd_finalize_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, partial, rows, C, K,
+                     dw, db, accum);
   return check_launch("outconv_bwd_finalize");
 }
 

@@ -35,7 +35,12 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
   constexpr int BCO = WCO * 64, BCI = WCI * 16;
   constexpr int HALO = (KS == 3) ? 1 : 0;
   constexpr int HWID = W2_TW + 2 * HALO, HHGT = W2_TH + 2 * HALO, HP = HWID * HHGT;
-  constexpr int RSX = BCI + 8, RSD = BCO + 8;  // LDS rows padded by 16 B
+  // LDS row strides are odd multiples of 32 B (16 bf16): the 4 rows a 16-lane group reads in one
+  // ds_read_b64_tr_b16 land on distinct 8-bank octets, and lane groups g = 1, 3 (which start 8 rows /
+  // pixels further, i.e. a multiple of 64 banks) read their "+4" half first (see the main loop), so the
+  // two groups served together hit disjoint octets: conflict-free
+  constexpr int RSX = BCI + (BCI % 32 == 0 ? 16 : 32), RSD = BCO + 16;
+  static_assert((RSX / 16) % 2 == 1 && (RSD / 16) % 2 == 1, "strides must be odd multiples of 32 B");
   constexpr int TAPS = KS * KS;
   constexpr int NVX = BCI / VEC, NVD = BCO / VEC;
   constexpr int IX = (HP * NVX + W2_NT - 1) / W2_NT;
@@ -59,7 +64,8 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
   make_view<T>(d, ci0 + vx * VEC, sv, sc, sf);
   const int cod = co0 + vd * VEC;
   const bool dy_ok = cod < d.Cout;
-  const char* dyb = (const char*)d.dy;
+  const char* dyb = (const char*)d.dy + (size_t)cod * sizeof(T);  // 32-bit offsets from here (host-checked)
+  const unsigned dy_pixb = (unsigned)d.Cout * sizeof(T);
 
   auto tile_nhw = [&](int mt, long long& n, int& h0, int& w0) {
     const int tw_i = mt % tiles_w;
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
       const int oh = h0 + p / W2_TW, ow = w0 + p % W2_TW;
       dq[k] = make_uint4(0, 0, 0, 0);
       if (dy_ok && p < W2_BM && oh < d.H && ow < d.W)
-        dq[k] = ld16<T>(dyb, ((n * d.H + oh) * (long long)d.W + ow) * d.Cout + cod);
+        dq[k] = ld16b(dyb, (((unsigned)n * d.H + oh) * d.W + ow) * dy_pixb);
     }
   };
   auto finish_d = [&](T* buf) {
@@ -110,7 +116,8 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
 #pragma unroll
     for (int k = 0; k < ID; ++k) {
       const int p = (tid + k * W2_NT) / NVD;
-      if (p < W2_BM) *reinterpret_cast<uint4*>(bd + p * RSD + vd * VEC) = dq[k];
+      // pixels of odd 8-blocks swap their 4-halves (the K permutation the halo reads apply, see below)
+      if (p < W2_BM) *reinterpret_cast<uint4*>(bd + (p ^ ((p & 8) >> 1)) * RSD + vd * VEC) = dq[k];
     }
   };
   auto issue = [&](int mt) {
@@ -153,9 +160,14 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
           if ((3 * k) / IX == s) issue_x(mt + 1, k);
       }
       // lane bases + compile-time offsets (so every LDS read is base + immediate): this lane addresses
-      // pixel rows pa = k0 + 8g + q and pa + 4; pixel pa sits at tile row 2s + (g>>1), column 8(g&1) + q
+      // pixel rows pa = k0 + 8g + q and pa + 4; pixel pa sits at tile row 2s + (g>>1), column 8(g&1) + q.
+      // Odd lane groups take the pa + 4 half as fragment elements 0..3 (bank spread, see RSX/RSD); A and
+      // B use the same K permutation (for dy it is built into the LDS row order by finish_d), so the
+      // products summed by the MFMA are unchanged.
+      const int sw = (g & 1) * 4;
       const T* dl = bd + (8 * g + q) * RSD + wco * 64 + p4;
-      const T* xl = bx + ((g >> 1) * HWID + 8 * (g & 1) + q) * RSX + wci * 16 + p4;
+      const T* xl0 = bx + ((g >> 1) * HWID + 8 * (g & 1) + q + sw) * RSX + wci * 16 + p4;
+      const T* xl1 = bx + ((g >> 1) * HWID + 8 * (g & 1) + q + 4 - sw) * RSX + wci * 16 + p4;
       bf16x8 a[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) a[i] = tr8(dl + k0 * RSD + i * 16, dl + (k0 + 4) * RSD + i * 16);
@@ -163,7 +175,7 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
       for (int t = 0; t < TAPS; ++t) {
         const int dy = t / KS, dx = t % KS;
         const int off = ((2 * s + dy) * HWID + dx) * RSX;
-        const bf16x8 b = tr8(xl + off, xl + off + 4 * RSX);
+        const bf16x8 b = tr8(xl0 + off, xl1 + off);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[t][i], 0, 0, 0);
       }
@@ -230,8 +242,10 @@ W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   for (int i = 0; i < d->nsrc; ++i) {
     const unet_src& s = d->src[i];
     if (s.kind == UNET_SRC_NCHW_F32 || (s.C % 8)) p.ok = false;
+    if ((double)d->N * s.H * s.W * s.C * 2 >= 4294967296.0) p.ok = false;  // 32-bit byte offsets
     if (s.kind == UNET_SRC_POOL_ACT || s.kind == UNET_SRC_UP_ACT) p.raw = 4;
   }
+  if ((double)d->N * d->H * d->W * d->Cout * 2 >= 4294967296.0) p.ok = false;
   if (!p.ok) return p;
   if (d->Cout <= 64) { p.wco = 1; p.wci = 4; } else { p.wco = 2; p.wci = 2; }
   const int bco = p.wco * 64, bci = p.wci * 16;
@@ -240,8 +254,10 @@ W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   p.mtiles = d->N * p.tiles_w * p.tiles_h;
   const long long tiles_out = (long long)cdiv(d->Cout, bco) * cdiv(d->Cin, bci);
   const size_t slab = (size_t)d->Cout * d->Cin * d->ksize * d->ksize * sizeof(float);
-  long long s = (512 + tiles_out - 1) / tiles_out;
-  const long long cap = (long long)(((size_t)96 << 20) / (slab ? slab : 1));
+  // one resident workgroup per CU (LDS ~90 KB): aim for one wave of 256 blocks, and keep the slab
+  // traffic (written once, read once by wgrad_reduce2) under ~32 MB
+  long long s = (256 + tiles_out - 1) / tiles_out;
+  const long long cap = (long long)(((size_t)32 << 20) / (slab ? slab : 1));
   if (s > cap) s = cap;
   if (s > p.mtiles) s = p.mtiles;
   if (s < 1) s = 1;
