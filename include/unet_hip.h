@@ -70,7 +70,7 @@ typedef struct unet_conv_desc {
   int ksize;              /* 1 or 3                                                               */
   int nsrc;               /* 1 or 2 (channel concat, src[0] first — layers.py:105,254)            */
   unet_src src[2];
-  const void* weight;     /* packed by unet_pack_weight: [Cout][ksize^2][Cin_pad]                 */
+  const void* weight;     /* packed by unet_pack_weight (fragment-major, see below)               */
   int out_mode;           /* UNET_OUT_*                                                           */
   void* out;              /* Y: op dtype [N,H,W,Cout]; F32: fp32 [N,H,W,split]                     */
   void* out2;             /* F32 split: fp32 [N,H,W,Cout-split]                                   */
@@ -102,7 +102,9 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len);
 
 /* ---- weights (nn.Conv2d weight OIHW fp32 -> packed operand) -------------------------------- */
 /* replaces the implicit weight read of nn.Conv2d — layers.py:32,35,120,152,158,164            */
-/* transpose=0: [Cout][k*k][Cin_pad] ; transpose=1 (dgrad): [Cin][k*k (flipped)][Cout_pad]      */
+/* fragment-major [Rpad/16][Kpad/KC][k*k][64 lanes][16 B], KC = 32 (bf16) / 16 (fp32), Rpad = R
+ * rounded up to 128.  transpose=0: rows R = Cout, reduction K = Cin (forward);
+ * transpose=1 (dgrad): rows R = Cin, reduction K = Cout, taps flipped 180 degrees               */
 int unet_pack_weight(int dtype, const float* w_oihw, void* packed, int Cout, int Cin, int ksize,
                      int transpose, void* stream);
 int unet_packed_weight_elems(int dtype, int Cout, int Cin, int ksize, int transpose);

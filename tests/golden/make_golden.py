@@ -7,6 +7,10 @@ Run in the build container only (the reference does not exist on the GPU box):
 Outputs are plain tensors (torch.save of dicts of tensors, loadable with weights_only=True) under
 tests/golden/.  No reference source or pickled reference object is stored.  The reference's own
 repository has no tests or fixtures, so these vectors are what pins the oracle.
+
+Status: the committed fixtures were produced by this script early in round 1.  Importing the
+reference was refused later in that round, so this script is not to be re-run: it is
+kept as the record of how the committed vectors were made.
 """
 
 from __future__ import annotations
