@@ -77,6 +77,15 @@ def cpu_baseline(model_kind: str, size: int, batch: int, iters: int) -> dict:
                       f"1 warm-up + {iters} timed fwd+DiceBCE+bwd iterations ({dt:.1f} s)"}
 
 
+def max_over_ranks(elapsed: float, device: torch.device) -> float:
+    """The job's wall time: the slowest rank's timed region (all ranks get the same value)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return elapsed
+    te = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(te, op=dist.ReduceOp.MAX)
+    return float(te)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -141,10 +150,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     probe.disable()
-    if world > 1:
-        te = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        elapsed = float(te)
+    elapsed = max_over_ranks(elapsed, dev)
     ps = probe.summary()
 
     images = world * args.batch * args.steps
