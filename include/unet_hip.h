@@ -60,7 +60,10 @@ typedef struct unet_src {
 enum {
   UNET_OUT_Y = 0,         /* store y (op dtype, NHWC) + per-tile BN partial sums                  */
   UNET_OUT_F32 = 1,       /* fp32 NHWC; split channels [0,split) -> out, [split,Cout) -> out2      */
-  UNET_OUT_POOL_BWD = 2   /* route to the 2x2 argmax of pool_src (ACT), add into out (fp32)        */
+  UNET_OUT_POOL_BWD = 2,  /* route to the 2x2 argmax of pool_src (ACT), add into out (fp32)        */
+  UNET_OUT_SHUFFLE2 = 3   /* ConvTranspose2d(k=2, s=2) as a 1x1 conv with Cout = 4*Ct: output channel
+                             (2a+b)*Ct + c of pixel (y, x) -> out[n, 2y+a, 2x+b, c] + bias[c]
+                             (op dtype [N,2H,2W,Ct])                         — layers.py:81,218   */
 };
 
 typedef struct unet_conv_desc {
@@ -78,6 +81,7 @@ typedef struct unet_conv_desc {
   int accum, accum2;      /* F32: add into out / out2 instead of storing                          */
   float* stats;           /* Y: [2][mtiles][Cout] partial sum / sum of squares (may be NULL)       */
   unet_src pool_src;      /* POOL_BWD: the pre-pool activation (kind ACT, H=2H', W=2W')           */
+  const float* bias;      /* SHUFFLE2: fp32 [Ct] (may be NULL)                                     */
 } unet_conv_desc;
 
 typedef struct unet_wgrad_desc {
@@ -175,6 +179,15 @@ int unet_resize_nchw(long long NC, int Hi, int Wi, int Ho, int Wo, float sh, flo
                      float* y, void* stream);
 int unet_resize_nchw_bwd(long long NC, int Hi, int Wi, int Ho, int Wo, float sh, float sw,
                          const float* dy, float* dx, int accum, void* stream);
+
+/* ---- ConvTranspose2d(k=2, s=2) backward helper — layers.py:81,218 ------------------------------ */
+/* d_up: fp32 NHWC [N,Hp,Wp,Ct] gradient at the padded up map (the transposed conv output sits at
+ * rows pad_t.., cols pad_l..).  Writes dy_s2d (op dtype [N,h,w,4*Ct], channel (2a+b)*Ct + c =
+ * d_up[n, pad_t+2y+a, pad_l+2x+b, c]) — the gradient of the equivalent 1x1 conv — and per-block
+ * bias partial sums partial[rows][Ct] (finish with unet_colsum).                                  */
+int unet_convt_bwd_rows(long long P);
+int unet_convt_bwd_prep(int dtype, long long N, int h, int w, int Ct, int Hp, int Wp, int pad_t, int pad_l,
+                        const float* d_up, void* dy_s2d, float* partial, void* stream);
 
 /* ---- OutConv (1x1 conv + bias, few classes) — layers.py:109-123 ------------------------------ */
 int unet_outconv_rows(long long P);

@@ -246,3 +246,44 @@ def test_first_conv_nchw_input(prec, shape):
     torch.cuda.synchronize()
     assert (dw - refw).abs().max() <= 1e-4 * (1 + refw.abs().max())
     del xr
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("shape", [(2, 8, 8, 64, 32, 0, 0), (1, 12, 20, 128, 64, 1, 2), (2, 5, 7, 32, 16, 0, 1)])
+def test_conv_transpose_k2s2(prec, shape):
+    """Up(bilinear=False): ConvTranspose2d(k=2, s=2, bias) as a 1x1 conv with the SHUFFLE2 epilogue,
+    and its backward (space-to-depth prep + bias colsum + 1x1 wgrad + 1x1 dgrad), vs torch fp32."""
+    from unet._hip.stages import ConvTStage, Grads
+    R = _rt()
+    P = R.BF16 if prec == "bf16" else R.FP32
+    N, h, w, cin, ct, pt, pl = shape
+    dt = DT[prec]
+    torch.manual_seed(5)
+    m = torch.nn.ConvTranspose2d(cin, ct, 2, 2).cuda()
+    with torch.no_grad():
+        m.weight.copy_(m.weight.to(dt).float())
+    y = _rand(N, h, w, cin, dt=dt)
+    ab = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2])
+    a = R.Act(y, ab, True)
+    st = ConvTStage(m)
+    u = st.forward(P, a)
+    x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = m(x)
+    tol = 2e-2 if prec == "bf16" else 1e-4
+    assert (u.data.float().permute(0, 3, 1, 2) - ref).abs().max() <= tol * (1 + ref.abs().max())
+    # backward through a padded placement
+    Hp, Wp = 2 * h + pt + 1, 2 * w + pl + 2
+    d_up = torch.zeros(N, Hp, Wp, ct, device="cuda")
+    g = torch.randn(N, 2 * h, 2 * w, ct, device="cuda").to(dt).float()
+    d_up[:, pt:pt + 2 * h, pl:pl + 2 * w] = g
+    grads = Grads()
+    st.backward(P, d_up, pt, pl, grads)
+    torch.cuda.synchronize()
+    ref.backward(g.permute(0, 3, 1, 2))
+    gw, gb = grads[m.weight], grads[m.bias]
+    assert gw.shape == m.weight.shape
+    tw = 1e-3 if prec == "bf16" else 1e-4
+    assert (gw - m.weight.grad).abs().max() <= tw * (1 + m.weight.grad.abs().max())
+    assert (gb - m.bias.grad).abs().max() <= 1e-4 * (1 + m.bias.grad.abs().max())
+    gx = x.grad.permute(0, 2, 3, 1)
+    assert (a.grad - gx).abs().max() <= tol * (1 + gx.abs().max())

@@ -9,8 +9,8 @@ from hip_helpers import build_model, grad_report, max_abs, rel_err
 
 pytestmark = pytest.mark.gpu
 
-MODULE_CASES = ["double_conv", "double_conv_mid", "down", "up_bilinear", "out_conv", "attention_gate",
-                "attention_gate_odd", "attention_up"]
+MODULE_CASES = ["double_conv", "double_conv_mid", "down", "up_bilinear", "up_transposed", "out_conv",
+                "attention_gate", "attention_gate_odd", "attention_up", "attention_up_transposed"]
 
 
 def _module_for(name, rec):
@@ -50,7 +50,8 @@ def test_module_fp32_vs_golden(golden_modules, name):
         assert max_abs(mine.float(), b.float()) <= 1e-4 * (1 + float(b.float().abs().max())), (name, k)
 
 
-MODEL_CASES = ["attention_unet_b8", "unet_b8", "attention_unet_b4_ds", "attention_unet_b4_odd"]
+MODEL_CASES = ["attention_unet_b8", "unet_b8", "attention_unet_b4_ds", "attention_unet_b4_odd", "unet_b4_transposed",
+               "attention_unet_b4_3ch_transposed"]
 
 
 @pytest.mark.parametrize("name", MODEL_CASES)

@@ -249,6 +249,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_des
         }
       }
     }
+  } else if (d.out_mode == UNET_OUT_SHUFFLE2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int oh = h0 + wm * 4 + i;
+#pragma unroll
+      for (int j = 0; j < NTN; ++j) {
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ow = ow_base + r;
+          if (oh < d.H && ow < d.W && co < d.Cout) store_shuffle2<T>(d, n, oh, ow, co, acc[i][j][r]);
+        }
+      }
+    }
   } else {  // UNET_OUT_POOL_BWD
     const unet_src& ps = d.pool_src;
     float* da = (float*)d.out;
@@ -470,6 +484,11 @@ int unet_conv(const unet_conv_desc* d, void* stream) {
   if (csum != d->Cin) { set_error("unet_conv: source channels != Cin"); return UNET_ERR_ARG; }
   if (d->out_mode == UNET_OUT_F32 && (d->split < 0 || d->split > d->Cout || (d->split < d->Cout && !d->out2))) {
     set_error("unet_conv: bad split");
+    return UNET_ERR_ARG;
+  }
+  if (d->out_mode < UNET_OUT_Y || d->out_mode > UNET_OUT_SHUFFLE2 ||
+      (d->out_mode == UNET_OUT_SHUFFLE2 && (d->Cout % 4 || d->ksize != 1))) {
+    set_error("unet_conv: bad out_mode");
     return UNET_ERR_ARG;
   }
   if (d->out_mode == UNET_OUT_POOL_BWD &&

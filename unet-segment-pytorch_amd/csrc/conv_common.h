@@ -26,6 +26,16 @@ template <> struct Mma<float> {
   }
 };
 
+// UNET_OUT_SHUFFLE2 epilogue store: the 1x1 conv's channel co = (2a+b)*Ct + c at input pixel (oh, ow)
+// is the ConvTranspose2d(k=2, s=2) output at (2*oh + a, 2*ow + b), channel c (+ bias)
+template <typename T>
+__device__ __forceinline__ void store_shuffle2(const unet_conv_desc& d, long long n, int oh, int ow, int co, float v) {
+  const int ct = d.Cout >> 2;
+  const int q = co / ct, c = co - q * ct;
+  const long long o = ((n * (2 * d.H) + 2 * oh + (q >> 1)) * (long long)(2 * d.W) + 2 * ow + (q & 1)) * ct + c;
+  reinterpret_cast<T*>(d.out)[o] = from_f<T>(v + (d.bias ? d.bias[c] : 0.f));
+}
+
 template <typename T> __host__ __device__ constexpr int kc_of() { return sizeof(T) == 2 ? 32 : 16; }
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 __device__ __forceinline__ int round_up_d(int a, int b) { return (a + b - 1) / b * b; }

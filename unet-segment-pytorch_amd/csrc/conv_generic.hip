@@ -163,6 +163,20 @@ __global__ __launch_bounds__(NTHR) void conv_generic_kernel(const unet_conv_desc
         }
       }
     }
+  } else if (d.out_mode == UNET_OUT_SHUFFLE2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int oh = h0 + wm * 4 + i;
+#pragma unroll
+      for (int j = 0; j < NTN; ++j) {
+        const int co = co0 + wn * (BN / 2) + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ow = ow_base + r;
+          if (oh < d.H && ow < d.W && co < d.Cout) store_shuffle2<T>(d, n, oh, ow, co, acc[i][j][r]);
+        }
+      }
+    }
   } else {  // UNET_OUT_POOL_BWD: gradient w.r.t. the pooled map -> 2x2 argmax of ACT(pool_src)
     const unet_src& ps = d.pool_src;
     float* da = (float*)d.out;

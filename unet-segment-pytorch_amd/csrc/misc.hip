@@ -356,6 +356,59 @@ __global__ void fill_kernel(float* x, long long n, float v) {
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) x[e] = v;
 }
 
+// ConvTranspose2d(k=2, s=2) backward prep: space-to-depth of the output gradient into the gradient of
+// the equivalent 1x1 conv (channel (2a+b)*Ct + c), plus per-block bias partial sums.
+// Block: CLN channel lanes x PL pixel lanes; one pixel range per block (fixed order -> deterministic).
+constexpr int CT_MAXCH = 4;  // channel chunks of 256 per thread (Ct <= 1024)
+template <typename T>
+__global__ __launch_bounds__(256) void convt_bwd_prep_kernel(long long N, int h, int w, int Ct, int Hp, int Wp, int pt,
+                                                             int pl, const float* d_up, T* out, float* partial,
+                                                             int rows) {
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  const int CLN = Ct < 256 ? Ct : 256, PL = 256 / CLN;
+  const int cl = tid % CLN, pq = tid / CLN;
+  const long long P = N * h * w;
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  float bs[CT_MAXCH];
+#pragma unroll
+  for (int k = 0; k < CT_MAXCH; ++k) bs[k] = 0.f;
+  if (pq < PL) {
+    for (long long p = p0 + pq; p < p1; p += PL) {
+      const int x = p % w;
+      const long long t = p / w;
+      const int y = t % h;
+      const long long n = t / h;
+#pragma unroll
+      for (int k = 0; k < CT_MAXCH; ++k) {
+        const int c = cl + k * CLN;
+        if (c < Ct) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const long long src = ((n * Hp + pt + 2 * y + (q >> 1)) * (long long)Wp + pl + 2 * x + (q & 1)) * Ct + c;
+            const float v = d_up[src];
+            out[p * 4 * Ct + q * Ct + c] = from_f<T>(v);
+            bs[k] += v;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CT_MAXCH; ++k) {
+    if (k * CLN >= Ct) break;
+    red[tid] = (pq < PL) ? bs[k] : 0.f;
+    __syncthreads();
+    if (tid < CLN && cl + k * CLN < Ct) {
+      float a = 0.f;
+      for (int q = 0; q < PL; ++q) a += red[q * CLN + tid];
+      partial[(size_t)blockIdx.x * Ct + cl + k * CLN] = a;
+    }
+    __syncthreads();
+  }
+}
+
 static inline int grid_for(long long total) {
   long long b = (total + 255) / 256;
   if (b > 8192) b = 8192;
@@ -492,6 +545,26 @@ int unet_gated_to_nchw(int dtype, long long N, int C, int H, int W, const void* 
     hipLaunchKernelGGL(gated_to_nchw_kernel<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H,
                        W, (const float*)x, scale, shift, relu, p, psi_ab, y);
   return check_launch("gated_to_nchw");
+}
+
+int unet_convt_bwd_rows(long long P) { return oc_rows(P); }
+
+int unet_convt_bwd_prep(int dtype, long long N, int h, int w, int Ct, int Hp, int Wp, int pad_t, int pad_l,
+                        const float* d_up, void* dy_s2d, float* partial, void* stream) {
+  if (N <= 0 || h <= 0 || w <= 0 || Ct <= 0 || Ct > 256 * CT_MAXCH || pad_t < 0 || pad_l < 0 ||
+      pad_t + 2 * h > Hp || pad_l + 2 * w > Wp) {
+    set_error("unet_convt_bwd_prep: bad geometry");
+    return UNET_ERR_ARG;
+  }
+  const int rows = oc_rows(N * h * w);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(convt_bwd_prep_kernel<bf16>, dim3(rows), dim3(256), 0, st, N, h, w, Ct, Hp, Wp, pad_t, pad_l,
+                       d_up, (bf16*)dy_s2d, partial, rows);
+  else
+    hipLaunchKernelGGL(convt_bwd_prep_kernel<float>, dim3(rows), dim3(256), 0, st, N, h, w, Ct, Hp, Wp, pad_t, pad_l,
+                       d_up, (float*)dy_s2d, partial, rows);
+  return check_launch("convt_bwd_prep");
 }
 
 int unet_fill_f32(float* x, long long n, float v, void* stream) {

@@ -16,7 +16,7 @@ _LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).resolve().parent 
 
 F32, BF16 = 0, 1
 SRC_PLAIN, SRC_ACT, SRC_POOL_ACT, SRC_UP_ACT, SRC_NCHW_F32, SRC_UP_PLAIN = range(6)
-OUT_Y, OUT_F32, OUT_POOL_BWD = range(3)
+OUT_Y, OUT_F32, OUT_POOL_BWD, OUT_SHUFFLE2 = range(4)
 
 c_int, c_ll, c_float, c_vp, c_size = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 
@@ -31,7 +31,7 @@ class ConvDesc(ctypes.Structure):
     _fields_ = [("dtype", c_int), ("N", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
                 ("ksize", c_int), ("nsrc", c_int), ("src", Src * 2), ("weight", c_vp), ("out_mode", c_int),
                 ("out", c_vp), ("out2", c_vp), ("split", c_int), ("accum", c_int), ("accum2", c_int),
-                ("stats", c_vp), ("pool_src", Src)]
+                ("stats", c_vp), ("pool_src", Src), ("bias", c_vp)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -73,6 +73,9 @@ _SIGS = {
                                   c_vp, c_vp, c_int, c_vp]),
     "unet_resize_nchw": (c_int, [c_ll, c_int, c_int, c_int, c_int, c_float, c_float, c_vp, c_vp, c_vp]),
     "unet_resize_nchw_bwd": (c_int, [c_ll, c_int, c_int, c_int, c_int, c_float, c_float, c_vp, c_vp, c_int, c_vp]),
+    "unet_convt_bwd_rows": (c_int, [c_ll]),
+    "unet_convt_bwd_prep": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                    c_vp]),
     "unet_outconv_rows": (c_int, [c_ll]),
     "unet_outconv_fwd": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
                                  c_vp]),

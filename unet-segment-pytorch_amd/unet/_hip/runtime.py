@@ -226,6 +226,14 @@ class Act:
         s.sw = up_scale(self.W, up_w)
         return s
 
+    def src_placed(self, pad_t: int, pad_l: int) -> L.Src:
+        """A plain stored map placed at (pad_t, pad_l) inside a larger conv input (F.pad of a
+        ConvTranspose2d output, layers.py:98-102)."""
+        assert self.ab is None
+        s = self._base(L.SRC_UP_PLAIN)
+        s.up_h, s.up_w, s.pad_t, s.pad_l = self.H, self.W, pad_t, pad_l
+        return s
+
     def src_gated(self, p: torch.Tensor, psi_ab: torch.Tensor) -> L.Src:
         s = self._base(L.SRC_ACT)
         s.gate_p = p.data_ptr()

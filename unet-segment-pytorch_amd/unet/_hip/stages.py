@@ -280,13 +280,97 @@ def _pad_geometry(x1: Act, x2: Act):
     return up_h, up_w, dy // 2, dx // 2     # F.pad([dx//2, dx-dx//2, dy//2, dy-dy//2]) — layers.py:101
 
 
+class ConvTStage:
+    """nn.ConvTranspose2d(Cin, Ct, kernel_size=2, stride=2) with bias — layers.py:81,218.
+
+    Run as a 1x1 conv with 4*Ct output channels (row (2a+b)*Ct + c of the reshaped weight is
+    W[:, c, a, b]) whose SHUFFLE2 epilogue scatters channel (a, b, c) of input pixel (y, x) to output
+    pixel (2y+a, 2x+b) and adds the bias.  Backward: space-to-depth of the output gradient
+    (unet_convt_bwd_prep, which also sums the bias gradient), then the ordinary 1x1 wgrad / dgrad."""
+
+    def __init__(self, m: torch.nn.ConvTranspose2d):
+        if m.kernel_size != (2, 2) or m.stride != (2, 2) or m.padding != (0, 0) or m.groups != 1 or \
+                m.dilation != (1, 1) or m.output_padding != (0, 0):
+            raise NotImplementedError("unet HIP path: only ConvTranspose2d(k=2, s=2) is supported")
+        self.m = m
+        self.cin, self.ct = m.in_channels, m.out_channels
+
+    def _w4(self) -> torch.Tensor:
+        return self.m.weight.detach().float().permute(2, 3, 1, 0).reshape(4 * self.ct, self.cin, 1, 1).contiguous()
+
+    def forward(self, prec, x1: Act) -> Act:
+        dev = x1.data.device
+        N, h, w = x1.N, x1.H, x1.W
+        self.x1 = x1
+        self.w4 = self._w4()
+        wp = pack_weight(self.w4, prec, transpose=False)
+        y = torch.empty(N, 2 * h, 2 * w, self.ct, dtype=prec.torch_dtype, device=dev)
+        d = _conv_desc(prec, N, h, w, self.cin, 4 * self.ct, 1, [x1.src()], wp)
+        d.out_mode = L.OUT_SHUFFLE2
+        d.out = y.data_ptr()
+        b = self.m.bias
+        self.bias = b.detach().float().contiguous() if b is not None else None
+        d.bias = vp(self.bias)
+        probe.launch(lambda: conv_kernel_name(d), 2.0 * N * h * w * self.cin * 4 * self.ct,
+                     lambda: L.call("unet_conv", d, stream()))
+        return Act(y, None, False)
+
+    def backward(self, prec, d_up: torch.Tensor, pad_t: int, pad_l: int, grads: Grads, need_dx: bool = True):
+        """d_up: fp32 NHWC gradient at the padded map that holds this output at (pad_t, pad_l)."""
+        x1 = self.x1
+        dev = x1.data.device
+        N, h, w, ct = x1.N, x1.H, x1.W, self.ct
+        P = N * h * w
+        dys = torch.empty(N, h, w, 4 * ct, dtype=prec.torch_dtype, device=dev)
+        rows = L.load().unet_convt_bwd_rows(P)
+        part = f32(rows, ct, device=dev)
+        L.call("unet_convt_bwd_prep", prec.code, N, h, w, ct, d_up.shape[1], d_up.shape[2], pad_t, pad_l, vp(d_up),
+               vp(dys), vp(part), stream())
+        if self.m.bias is not None:
+            db = f32(ct, device=dev)
+            L.call("unet_colsum", vp(part), rows, ct, vp(db), 0, stream())
+            grads.put(self.m.bias, db)
+        # weight gradient of the equivalent 1x1 conv, back to the ConvTranspose2d layout [Cin][Ct][2][2]
+        wd = L.WgradDesc()
+        wd.dtype = prec.code
+        wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize = N, h, w, self.cin, 4 * ct, 1
+        wd.nsrc = 1
+        wd.src[0] = x1.src()
+        wd.dy = dys.data_ptr()
+        dw4 = f32(4 * ct, self.cin, device=dev)
+        wd.dw = dw4.data_ptr()
+        wd.accum = 0
+        ws = torch.empty(max(L.load().unet_wgrad_workspace(wd), 16), dtype=torch.uint8, device=dev)
+        wd.workspace = ws.data_ptr()
+        probe.launch(lambda: wgrad_kernel_name(prec, 1), 2.0 * P * self.cin * 4 * ct,
+                     lambda: L.call("unet_conv_wgrad", wd, stream()))
+        grads.put(self.m.weight, dw4.view(2, 2, ct, self.cin).permute(3, 2, 0, 1).contiguous())
+        if not need_dx:
+            return
+        wt = pack_weight(self.w4, prec, transpose=True)
+        d = _conv_desc(prec, N, h, w, 4 * ct, self.cin, 1, [_plain_src(dys)], wt)
+        d.out_mode = L.OUT_F32
+        g, acc = x1.grad_target()
+        d.out = g.data_ptr()
+        d.accum = acc
+        d.split = self.cin
+        probe.launch(lambda: conv_kernel_name(d), 2.0 * P * self.cin * 4 * ct,
+                     lambda: L.call("unet_conv", d, stream()))
+
+
 class UpStage:
-    """Up (layers.py:64-106) and AttentionUp (layers.py:195-255), bilinear=True:
-    [skip (· attention), pad(up(x1))] -> DoubleConv, with the concat/pad/upsample virtual."""
+    """Up (layers.py:64-106) and AttentionUp (layers.py:195-255):
+    [skip (· attention), pad(up(x1))] -> DoubleConv, with the concat/pad (and bilinear upsample)
+    virtual.  bilinear=False runs the ConvTranspose2d as its own stage (ConvTStage) whose output is
+    read in place by the DoubleConv's loader."""
 
     def __init__(self, m, attention: bool):
-        if not isinstance(m.up, torch.nn.Upsample):
-            raise NotImplementedError("unet HIP path: bilinear=False (ConvTranspose2d up) is not implemented yet")
+        if isinstance(m.up, torch.nn.Upsample):
+            self.convt = None
+        elif isinstance(m.up, torch.nn.ConvTranspose2d):
+            self.convt = ConvTStage(m.up)
+        else:
+            raise NotImplementedError(f"unet HIP path: unsupported up module {type(m.up).__name__}")
         self.dc = DoubleConvStage(m.conv)
         self.gate = GateStage(m.attention) if attention else None
 
@@ -299,19 +383,24 @@ class UpStage:
             skip = self.gate.gated_src()
         else:
             skip = x2.src()
-        srcs = [skip, x1.src_up(up_h, up_w, pt, pl)]
-        return self.dc.forward(prec, srcs, x2.N, x2.H, x2.W, training)
+        if self.convt is not None:
+            self.u = self.convt.forward(prec, x1)
+            up = self.u.src_placed(pt, pl)
+        else:
+            up = x1.src_up(up_h, up_w, pt, pl)
+        return self.dc.forward(prec, [skip, up], x2.N, x2.H, x2.W, training)
 
     def backward(self, prec, grads: Grads):
         x1, x2 = self.x1, self.x2
         dev = x2.data.device
         up_h, up_w, pt, pl = self.geo
-        d_up = f32(x2.N, x2.H, x2.W, x1.C, device=dev)
+        cu = self.convt.ct if self.convt is not None else x1.C
+        d_up = f32(x2.N, x2.H, x2.W, cu, device=dev)
         if self.gate is not None:
             d_xs = f32(x2.N, x2.H, x2.W, x2.C, device=dev)
             self.dc.backward(prec, grads, {"mode": "f32", "out": d_xs, "accum": 0, "out2": d_up, "accum2": 0,
                                            "split": x2.C})
-            same = (up_h == x2.H and up_w == x2.W and pt == 0 and pl == 0)
+            same = (self.convt is None and up_h == x2.H and up_w == x2.W and pt == 0 and pl == 0)
             if same:
                 self.gate.backward(prec, d_xs, grads, d_up, 1)
             else:
@@ -324,6 +413,9 @@ class UpStage:
             g2, acc2 = x2.grad_target()
             self.dc.backward(prec, grads, {"mode": "f32", "out": g2, "accum": acc2, "out2": d_up, "accum2": 0,
                                            "split": x2.C})
+        if self.convt is not None:
+            self.convt.backward(prec, d_up, pt, pl, grads)
+            return
         gx, acc = x1.grad_target()
         L.call("unet_upsample_bwd", x1.N, x1.C, x1.H, x1.W, up_h, up_w, pt, pl, x2.H, x2.W,
                up_scale(x1.H, up_h), up_scale(x1.W, up_w), vp(d_up), vp(gx), acc, stream())
