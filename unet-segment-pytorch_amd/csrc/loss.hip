@@ -71,21 +71,31 @@ __global__ void loss_reduce_kernel(long long N, int K_, long long HW, const floa
   }
 }
 
-// one block, one thread per image; then thread 0 combines
+// one block: (1) one wave per (image, field) pair sums the partial rows in fp64 (fixed order per
+// lane, then a fixed shuffle tree); (2) one thread per image forms its terms; (3) thread 0 combines
 // coef layout [N][2 + 2K]: w0, w1, gA[K], gB[K]
 __global__ void loss_finalize_kernel(const float* part, int rows, long long N, int K, float ce_w, float dice_w,
                                      float class_w, float ce_smooth, float dice_smooth, int ignore_bg, int reduction,
                                      float* loss, float* coef) {
-  extern __shared__ double dsh[];  // [N] ce terms, [N*K] dice terms
+  extern __shared__ double dsh[];  // [N] ce terms, [N*K] dice terms, [N*F] field sums
   const int F = 4 + 3 * K;
   const int c_lo = (ignore_bg && K > 1) ? 1 : 0;
   const int nd = K - c_lo;
   const double wred = reduction == 0 ? 1.0 / ((double)N * nd) : 1.0;  // mean / sum / none(=1, gout per elem)
+  double* fs = dsh + N + N * K;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (long long pf = wave; pf < N * F; pf += nw) {
+    const long long n = pf / F;
+    const int f = (int)(pf % F);
+    double a = 0;
+    for (int r = lane; r < rows; r += 64) a += part[((size_t)n * rows + r) * F + f];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (lane == 0) fs[pf] = a;
+  }
+  __syncthreads();
   for (long long n = threadIdx.x; n < N; n += blockDim.x) {
-    double s[4 + 3 * LMAXK];
-    for (int f = 0; f < F; ++f) s[f] = 0;
-    for (int r = 0; r < rows; ++r)
-      for (int f = 0; f < F; ++f) s[f] += part[((size_t)n * rows + r) * F + f];
+    const double* s = fs + n * F;
     const double n0 = (double)(float)(s[0]) + ce_smooth, n1 = (double)(float)(s[1]) + ce_smooth;
     const double w0 = (1.0 - class_w) / n0, w1 = class_w / n1;
     dsh[n] = w0 * s[2] + w1 * s[3];
@@ -193,9 +203,9 @@ int unet_loss_reduce(long long N, int K, long long HW, const float* z, const int
 int unet_loss_finalize(const float* partial, int rows, long long N, int K, float ce_w, float dice_w, float class_w,
                        float ce_smooth, float dice_smooth, int ignore_bg, int reduction, float* loss, float* coef,
                        void* stream) {
-  const size_t shm = (size_t)(N + N * K) * sizeof(double);
+  const size_t shm = (size_t)(N + N * K + N * (4 + 3 * K)) * sizeof(double);
   if (shm > 60000) { set_error("unet_loss_finalize: batch too large"); return UNET_ERR_UNSUPPORTED; }
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), shm, (hipStream_t)stream, partial, rows, N, K, ce_w,
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), shm, (hipStream_t)stream, partial, rows, N, K, ce_w,
                      dice_w, class_w, ce_smooth, dice_smooth, ignore_bg, reduction, loss, coef);
   return check_launch("loss_finalize");
 }

@@ -17,7 +17,7 @@
 
 namespace unet {
 
-constexpr int W2_TH = 8, W2_TW = 16, W2_BM = 128, W2_NT = 256;
+constexpr int W2_TH = 8, W2_TW = 16, W2_BM = 128;
 
 __device__ __forceinline__ bf16x8 tr8(const bf16* r0, const bf16* r1) {
   const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r0));
@@ -27,12 +27,13 @@ __device__ __forceinline__ bf16x8 tr8(const bf16* r0, const bf16* r1) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
-template <int KS, int WCO, int WCI, int RAW>
-__global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, int tiles_w, int tiles_h, int mtiles,
+template <int KS, int WCO, int WCI, int MI, int RAW>
+__global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad_desc d, int tiles_w, int tiles_h, int mtiles,
                                                       int per_split, float* ws) {
   using T = bf16;
+  constexpr int W2_NT = 64 * WCO * WCI;
   constexpr int VEC = 8;
-  constexpr int BCO = WCO * 64, BCI = WCI * 16;
+  constexpr int BCO = WCO * 16 * MI, BCI = WCI * 16;
   constexpr int HALO = (KS == 3) ? 1 : 0;
   constexpr int HWID = W2_TW + 2 * HALO, HHGT = W2_TH + 2 * HALO, HP = HWID * HHGT;
   // LDS row strides are odd multiples of 32 B (16 bf16): the 4 rows a 16-lane group reads in one
@@ -131,11 +132,11 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
     finish_d(buf);
   };
 
-  f32x4 acc[TAPS][4];
+  f32x4 acc[TAPS][MI];
 #pragma unroll
   for (int t = 0; t < TAPS; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < MI; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (mt_begin < mt_end) {
     issue(mt_begin);
@@ -153,11 +154,23 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
 #pragma unroll
     for (int k0 = 0; k0 < W2_BM; k0 += 32) {
       const int s = k0 / 32;  // K step 0..3
+      // next tile's raw loads: all issued at K-step 0 (x) / 1 (dy) and consumed after K-steps 2-3,
+      // so two to three K-steps of MFMAs cover their latency
+      // (RAW=4 sources keep the shorter one-K-step window: their 4-corner loads and max/bilinear
+      // transforms measured faster spread over all four K-steps)
       if (has_next) {
-        if (s == 0) issue_d(mt + 1);
+        if constexpr (RAW == 1) {
+          if (s == 0) {
 #pragma unroll
-        for (int k = 0; k < IX; ++k)
-          if ((3 * k) / IX == s) issue_x(mt + 1, k);
+            for (int k = 0; k < IX; ++k) issue_x(mt + 1, k);
+          }
+          if (s == 1) issue_d(mt + 1);
+        } else {
+          if (s == 0) issue_d(mt + 1);
+#pragma unroll
+          for (int k = 0; k < IX; ++k)
+            if ((3 * k) / IX == s) issue_x(mt + 1, k);
+        }
       }
       // lane bases + compile-time offsets (so every LDS read is base + immediate): this lane addresses
       // pixel rows pa = k0 + 8g + q and pa + 4; pixel pa sits at tile row 2s + (g>>1), column 8(g&1) + q.
@@ -165,25 +178,32 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
       // B use the same K permutation (for dy it is built into the LDS row order by finish_d), so the
       // products summed by the MFMA are unchanged.
       const int sw = (g & 1) * 4;
-      const T* dl = bd + (8 * g + q) * RSD + wco * 64 + p4;
+      const T* dl = bd + (8 * g + q) * RSD + wco * 16 * MI + p4;
       const T* xl0 = bx + ((g >> 1) * HWID + 8 * (g & 1) + q + sw) * RSX + wci * 16 + p4;
       const T* xl1 = bx + ((g >> 1) * HWID + 8 * (g & 1) + q + 4 - sw) * RSX + wci * 16 + p4;
-      bf16x8 a[4];
+      bf16x8 a[MI];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = tr8(dl + k0 * RSD + i * 16, dl + (k0 + 4) * RSD + i * 16);
+      for (int i = 0; i < MI; ++i) a[i] = tr8(dl + k0 * RSD + i * 16, dl + (k0 + 4) * RSD + i * 16);
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) {
         const int dy = t / KS, dx = t % KS;
         const int off = ((2 * s + dy) * HWID + dx) * RSX;
         const bf16x8 b = tr8(xl0 + off, xl1 + off);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[t][i], 0, 0, 0);
+        for (int i = 0; i < MI; ++i) acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[t][i], 0, 0, 0);
       }
       if (has_next) {
-        if (s == 1) finish_d(nb);
+        if constexpr (RAW == 1) {
 #pragma unroll
-        for (int k = 0; k < IX; ++k)
-          if ((3 * k) / IX + 1 == s) finish_x(mt + 1, k, nb);
+          for (int k = 0; k < IX; ++k)
+            if (s == 2 + (k * 2) / IX) finish_x(mt + 1, k, nb);
+          if (s == 3) finish_d(nb);
+        } else {
+          if (s == 1) finish_d(nb);
+#pragma unroll
+          for (int k = 0; k < IX; ++k)
+            if ((3 * k) / IX + 1 == s) finish_x(mt + 1, k, nb);
+        }
       }
     }
     __syncthreads();
@@ -195,10 +215,10 @@ __global__ __launch_bounds__(W2_NT) void wgrad2_kernel(const unet_wgrad_desc d, 
 #pragma unroll
   for (int t = 0; t < TAPS; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const int co = co0 + wco * 16 * MI + i * 16 + 4 * (lane >> 4) + r;
         if (co < d.Cout && ci < d.Cin) slab[((size_t)co * d.Cin + ci) * TAPS + t] = acc[t][i][r];
       }
 }
@@ -231,7 +251,7 @@ __global__ void wgrad_reduce2_kernel(const float* ws, int splits, long long tota
 
 struct W2Plan {
   bool ok;
-  int wco, wci, raw, tiles_w, tiles_h, mtiles, splits, per_split;
+  int wco, wci, mi, raw, tiles_w, tiles_h, mtiles, splits, per_split;
   size_t ws_bytes;
 };
 
@@ -247,17 +267,24 @@ W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   }
   if ((double)d->N * d->H * d->W * d->Cout * 2 >= 4294967296.0) p.ok = false;
   if (!p.ok) return p;
-  if (d->Cout <= 64) { p.wco = 1; p.wci = 4; } else { p.wco = 2; p.wci = 2; }
-  const int bco = p.wco * 64, bci = p.wci * 16;
+  // 8 waves (2 per SIMD: one wave's staging VALU runs beside the other's MFMAs) when Cin fills BCI=64
+  // wave tile = (16*MI co) x 16 ci x k*k taps.  3x3, Cout > 64: 8 waves of 32co (2 per SIMD, so one
+  // wave's staging VALU runs beside the other's MFMAs; 72 accumulators fit the 256-VGPR budget)
+  // (RAW=4 sources keep 4 waves: their staging registers do not fit beside 72 accumulators at 2/SIMD)
+  if (d->Cout <= 64) { p.wco = 1; p.wci = 4; p.mi = 4; }
+  else if (d->ksize == 3 && p.raw == 1) { p.wco = 4; p.wci = 2; p.mi = 2; }
+  else if (d->Cin >= 64) { p.wco = 2; p.wci = 4; p.mi = 4; }
+  else { p.wco = 2; p.wci = 2; p.mi = 4; }
+  const int bco = p.wco * 16 * p.mi, bci = p.wci * 16;
   p.tiles_w = cdiv(d->W, W2_TW);
   p.tiles_h = cdiv(d->H, W2_TH);
   p.mtiles = d->N * p.tiles_w * p.tiles_h;
   const long long tiles_out = (long long)cdiv(d->Cout, bco) * cdiv(d->Cin, bci);
   const size_t slab = (size_t)d->Cout * d->Cin * d->ksize * d->ksize * sizeof(float);
-  // one resident workgroup per CU (LDS ~90 KB): aim for one wave of 256 blocks, and keep the slab
-  // traffic (written once, read once by wgrad_reduce2) under ~32 MB
+  // one resident workgroup per CU (LDS 98-131 KB): aim for at least one wave of 256 blocks; the slab
+  // traffic (written once, read once by wgrad_reduce2, ~25 us per 150 MB) is capped at 160 MB
   long long s = (256 + tiles_out - 1) / tiles_out;
-  const long long cap = (long long)(((size_t)32 << 20) / (slab ? slab : 1));
+  const long long cap = (long long)(((size_t)160 << 20) / (slab ? slab : 1));
   if (s > cap) s = cap;
   if (s > p.mtiles) s = p.mtiles;
   if (s < 1) s = 1;
@@ -267,18 +294,24 @@ W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   return p;
 }
 
-template <int KS, int WCO, int WCI, int RAW>
+template <int KS, int WCO, int WCI, int MI, int RAW>
 static int launch_w2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
-  dim3 grid(p.splits, cdiv(d->Cin, WCI * 16), cdiv(d->Cout, WCO * 64));
-  hipLaunchKernelGGL((wgrad2_kernel<KS, WCO, WCI, RAW>), grid, dim3(W2_NT), 0, st, *d, p.tiles_w, p.tiles_h, p.mtiles,
+  dim3 grid(p.splits, cdiv(d->Cin, WCI * 16), cdiv(d->Cout, WCO * 16 * MI));
+  hipLaunchKernelGGL((wgrad2_kernel<KS, WCO, WCI, MI, RAW>), grid, dim3(64 * WCO * WCI), 0, st, *d, p.tiles_w, p.tiles_h, p.mtiles,
                      p.per_split, (float*)d->workspace);
   return check_launch("wgrad2");
 }
 
 template <int KS, int RAW>
 static int launch_w2_cfg(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
-  if (p.wco == 1) return launch_w2<KS, 1, 4, RAW>(d, p, st);
-  return launch_w2<KS, 2, 2, RAW>(d, p, st);
+  if (p.wco == 1) return launch_w2<KS, 1, 4, 4, RAW>(d, p, st);
+  if constexpr (KS == 3 && RAW == 1) {
+    if (p.wco == 4) return launch_w2<KS, 4, 2, 2, RAW>(d, p, st);
+  }
+  if constexpr (KS == 1) {
+    if (p.wci == 4) return launch_w2<KS, 2, 4, 4, RAW>(d, p, st);
+  }
+  return launch_w2<KS, 2, 2, 4, RAW>(d, p, st);
 }
 
 int launch_wgrad2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
