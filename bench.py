@@ -137,7 +137,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    target = args.probe or f"conv2_kernel<{args.precision},3,4,2,4,1>"
+    target = args.probe or ("conv3_kernel<bf16,3,2,4,2,8,1>" if args.precision == "bf16" else "conv2_kernel<fp32,3,4,2,4,1>")
     probe.enable(target)
     if world > 1:
         dist.barrier()

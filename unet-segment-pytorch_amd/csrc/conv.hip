@@ -23,6 +23,140 @@ constexpr int CTW = 16;          // tile width in pixels
 constexpr int PACK_NPAD = 128;   // packed rows padded to the largest BN
 
 // ------------------------------------------------------------------------------------------------
+// epilogue shared by conv2 / conv3.  acc[i][j][r] (lane l): pixel (h0 + MI*wm + i, w0 + 4*(l>>4) + r),
+// channel co0 + (wn*NTN + j)*16 + (l&15).  Modes: y + BN partial sums, fp32 (split across the concat,
+// optionally accumulated), ConvTranspose2d shuffle, max-pool backward routing.
+template <typename T, int WM, int WN, int NTN, int MI = 4>
+__device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&acc)[MI][NTN], T* lds, int tid,
+                                              int lane, int wm, int wn, long long n, int h0, int w0, int co0,
+                                              int mt, int mtiles) {
+  constexpr int BN = WN * NTN * 16;
+  // acc[i][j][r] (lane l): pixel (h0 + MI*wm + i, w0 + 4*(l>>4) + r), channel co0 + (wn*NTN + j)*16 + (l&15)
+  const int ow_base = w0 + 4 * (lane >> 4);
+  if (d.out_mode == UNET_OUT_Y) {
+    T* y = (T*)d.out;
+    float s[NTN], ss[NTN];
+#pragma unroll
+    for (int j = 0; j < NTN; ++j) { s[j] = 0.f; ss[j] = 0.f; }
+#pragma unroll MI
+    for (int i = 0; i < MI; ++i) {
+      const int oh = h0 + wm * MI + i;
+#pragma unroll NTN
+      for (int j = 0; j < NTN; ++j) {
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
+#pragma unroll 4
+        for (int r = 0; r < 4; ++r) {
+          const int ow = ow_base + r;
+          if (oh < d.H && ow < d.W && co < d.Cout) {
+            const float val = acc[i][j][r];
+            y[((n * d.H + oh) * (long long)d.W + ow) * d.Cout + co] = from_f<T>(val);
+            s[j] += val;
+            ss[j] += val * val;
+          }
+        }
+      }
+    }
+    if (d.stats) {
+      float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
+#pragma unroll NTN
+      for (int j = 0; j < NTN; ++j) {
+        s[j] += __shfl_xor(s[j], 16, 64);
+        s[j] += __shfl_xor(s[j], 32, 64);
+        ss[j] += __shfl_xor(ss[j], 16, 64);
+        ss[j] += __shfl_xor(ss[j], 32, 64);
+        if (lane < 16) {
+          const int col = (wn * NTN + j) * 16 + lane;
+          red[(wm * BN + col) * 2 + 0] = s[j];
+          red[(wm * BN + col) * 2 + 1] = ss[j];
+        }
+      }
+      __syncthreads();
+      if (tid < BN) {
+        const int co = co0 + tid;
+        if (co < d.Cout) {
+          float a = 0.f, b = 0.f;
+#pragma unroll
+          for (int w = 0; w < WM; ++w) { a += red[(w * BN + tid) * 2]; b += red[(w * BN + tid) * 2 + 1]; }
+          d.stats[(size_t)mt * d.Cout + co] = a;
+          d.stats[((size_t)mtiles + mt) * d.Cout + co] = b;
+        }
+      }
+    }
+  } else if (d.out_mode == UNET_OUT_F32) {
+    float* o1 = (float*)d.out;
+    float* o2 = (float*)d.out2;
+    const int c2 = d.Cout - d.split;
+#pragma unroll MI
+    for (int i = 0; i < MI; ++i) {
+      const int oh = h0 + wm * MI + i;
+#pragma unroll NTN
+      for (int j = 0; j < NTN; ++j) {
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
+#pragma unroll 4
+        for (int r = 0; r < 4; ++r) {
+          const int ow = ow_base + r;
+          if (oh < d.H && ow < d.W && co < d.Cout) {
+            const long long pix = (n * d.H + oh) * (long long)d.W + ow;
+            const float val = acc[i][j][r];
+            if (co < d.split) {
+              float* p = o1 + pix * d.split + co;
+              *p = d.accum ? *p + val : val;
+            } else {
+              float* p = o2 + pix * c2 + (co - d.split);
+              *p = d.accum2 ? *p + val : val;
+            }
+          }
+        }
+      }
+    }
+  } else if (d.out_mode == UNET_OUT_SHUFFLE2) {
+#pragma unroll MI
+    for (int i = 0; i < MI; ++i) {
+      const int oh = h0 + wm * MI + i;
+#pragma unroll NTN
+      for (int j = 0; j < NTN; ++j) {
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
+#pragma unroll 4
+        for (int r = 0; r < 4; ++r) {
+          const int ow = ow_base + r;
+          if (oh < d.H && ow < d.W && co < d.Cout) store_shuffle2<T>(d, n, oh, ow, co, acc[i][j][r]);
+        }
+      }
+    }
+  } else {  // UNET_OUT_POOL_BWD
+    const unet_src& ps = d.pool_src;
+    float* da = (float*)d.out;
+    const T* ysrc = (const T*)ps.data;
+#pragma unroll MI
+    for (int i = 0; i < MI; ++i) {
+      const int oh = h0 + wm * MI + i;
+#pragma unroll NTN
+      for (int j = 0; j < NTN; ++j) {
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
+#pragma unroll 4
+        for (int r = 0; r < 4; ++r) {
+          const int ow = ow_base + r;
+          if (oh < d.H && ow < d.W && co < d.Cout) {
+            const float scv = ps.scale[co], sfv = ps.shift[co];
+            float best = -INFINITY;
+            int bq = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const long long sp = (n * ps.H + 2 * oh + (q >> 1)) * (long long)ps.W + 2 * ow + (q & 1);
+              float a = to_f(ysrc[sp * d.Cout + co]) * scv + sfv;
+              if (ps.relu) a = fmaxf(a, 0.f);
+              if (a > best || a != a) { best = a; bq = q; }
+            }
+            const long long sp = (n * ps.H + 2 * oh + (bq >> 1)) * (long long)ps.W + 2 * ow + (bq & 1);
+            da[sp * d.Cout + co] += acc[i][j][r];
+          }
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 template <typename T, int KS, int WM, int WN, int NTN, int RAW>
 __global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_desc d, int tiles_w, int tiles_h,
                                                              int mtiles, int nchunks) {
@@ -170,130 +304,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_des
     __syncthreads();
   }
 
-  // ---- epilogue ----
-  // acc[i][j][r] (lane l): pixel (h0 + 4*wm + i, w0 + 4*(l>>4) + r), channel co0 + (wn*NTN + j)*16 + (l&15)
-  const int ow_base = w0 + 4 * (lane >> 4);
-  if (d.out_mode == UNET_OUT_Y) {
-    T* y = (T*)d.out;
-    float s[NTN], ss[NTN];
-#pragma unroll
-    for (int j = 0; j < NTN; ++j) { s[j] = 0.f; ss[j] = 0.f; }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int oh = h0 + wm * 4 + i;
-#pragma unroll
-      for (int j = 0; j < NTN; ++j) {
-        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ow = ow_base + r;
-          if (oh < d.H && ow < d.W && co < d.Cout) {
-            const float val = acc[i][j][r];
-            y[((n * d.H + oh) * (long long)d.W + ow) * d.Cout + co] = from_f<T>(val);
-            s[j] += val;
-            ss[j] += val * val;
-          }
-        }
-      }
-    }
-    if (d.stats) {
-      float* red = reinterpret_cast<float*>(lds);  // [WM][BN][2]
-#pragma unroll
-      for (int j = 0; j < NTN; ++j) {
-        s[j] += __shfl_xor(s[j], 16, 64);
-        s[j] += __shfl_xor(s[j], 32, 64);
-        ss[j] += __shfl_xor(ss[j], 16, 64);
-        ss[j] += __shfl_xor(ss[j], 32, 64);
-        if (lane < 16) {
-          const int col = (wn * NTN + j) * 16 + lane;
-          red[(wm * BN + col) * 2 + 0] = s[j];
-          red[(wm * BN + col) * 2 + 1] = ss[j];
-        }
-      }
-      __syncthreads();
-      if (tid < BN) {
-        const int co = co0 + tid;
-        if (co < d.Cout) {
-          float a = 0.f, b = 0.f;
-#pragma unroll
-          for (int w = 0; w < WM; ++w) { a += red[(w * BN + tid) * 2]; b += red[(w * BN + tid) * 2 + 1]; }
-          d.stats[(size_t)mt * d.Cout + co] = a;
-          d.stats[((size_t)mtiles + mt) * d.Cout + co] = b;
-        }
-      }
-    }
-  } else if (d.out_mode == UNET_OUT_F32) {
-    float* o1 = (float*)d.out;
-    float* o2 = (float*)d.out2;
-    const int c2 = d.Cout - d.split;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int oh = h0 + wm * 4 + i;
-#pragma unroll
-      for (int j = 0; j < NTN; ++j) {
-        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ow = ow_base + r;
-          if (oh < d.H && ow < d.W && co < d.Cout) {
-            const long long pix = (n * d.H + oh) * (long long)d.W + ow;
-            const float val = acc[i][j][r];
-            if (co < d.split) {
-              float* p = o1 + pix * d.split + co;
-              *p = d.accum ? *p + val : val;
-            } else {
-              float* p = o2 + pix * c2 + (co - d.split);
-              *p = d.accum2 ? *p + val : val;
-            }
-          }
-        }
-      }
-    }
-  } else if (d.out_mode == UNET_OUT_SHUFFLE2) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int oh = h0 + wm * 4 + i;
-#pragma unroll
-      for (int j = 0; j < NTN; ++j) {
-        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ow = ow_base + r;
-          if (oh < d.H && ow < d.W && co < d.Cout) store_shuffle2<T>(d, n, oh, ow, co, acc[i][j][r]);
-        }
-      }
-    }
-  } else {  // UNET_OUT_POOL_BWD
-    const unet_src& ps = d.pool_src;
-    float* da = (float*)d.out;
-    const T* ysrc = (const T*)ps.data;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int oh = h0 + wm * 4 + i;
-#pragma unroll
-      for (int j = 0; j < NTN; ++j) {
-        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ow = ow_base + r;
-          if (oh < d.H && ow < d.W && co < d.Cout) {
-            const float scv = ps.scale[co], sfv = ps.shift[co];
-            float best = -INFINITY;
-            int bq = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const long long sp = (n * ps.H + 2 * oh + (q >> 1)) * (long long)ps.W + 2 * ow + (q & 1);
-              float a = to_f(ysrc[sp * d.Cout + co]) * scv + sfv;
-              if (ps.relu) a = fmaxf(a, 0.f);
-              if (a > best || a != a) { best = a; bq = q; }
-            }
-            const long long sp = (n * ps.H + 2 * oh + (bq >> 1)) * (long long)ps.W + 2 * ow + (bq & 1);
-            da[sp * d.Cout + co] += acc[i][j][r];
-          }
-        }
-      }
-    }
-  }
+  conv_epilogue<T, WM, WN, NTN>(d, acc, lds, tid, lane, wm, wn, n, h0, w0, co0, mt, mtiles);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -343,6 +354,8 @@ static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t s
   return launch_conv2<T, KS, 2, 4, 2, RAW>(d, st);
 }
 
+#include "conv3_body.inc"
+
 template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
 bool smallcin_conv_ok(const unet_conv_desc* d);  // smallcin.hip
 int smallcin_rows(long long P);
@@ -365,6 +378,7 @@ template <typename T>
 static int dispatch_conv(const unet_conv_desc* d, hipStream_t st) {
   if (!fast_eligible(d)) return dispatch_generic<T>(d, st);
   const ConvCfg c = pick_cfg(d);
+  if (conv3_eligible(d)) return dispatch_conv3(d, c, st);
   if (d->ksize == 3) return c.raw == 4 ? dispatch_cfg<T, 3, 4>(d, c, st) : dispatch_cfg<T, 3, 1>(d, c, st);
   return c.raw == 4 ? dispatch_cfg<T, 1, 4>(d, c, st) : dispatch_cfg<T, 1, 1>(d, c, st);
 }
@@ -433,8 +447,15 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
     return 0;
   }
   const ConvCfg c = pick_cfg(d);
-  snprintf(buf, len, "conv2_kernel<%s,%d,%d,%d,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize, c.wm,
-           c.wn, c.ntn, c.raw);
+  if (conv3_eligible(d)) {
+    // the (wm, wn, ntn) block tile of pick_cfg; 16-row tiles run as MI=8 waves (dispatch_conv3)
+    const bool mi8 = c.raw == 1 && c.wm == 4 && (c.ntn == 4 || c.ntn == 2);
+    snprintf(buf, len, "conv3_kernel<bf16,3,%d,%d,%d,%d,%d>", mi8 ? 2 : c.wm, mi8 ? 4 : c.wn, mi8 ? c.ntn / 2 : c.ntn,
+             mi8 ? 8 : 4, c.raw);
+    return 0;
+  }
+  snprintf(buf, len, "conv2_kernel<%s,%d,%d,%d,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize, c.wm, c.wn,
+           c.ntn, c.raw);
   return 0;
 }
 
