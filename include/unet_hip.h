@@ -112,6 +112,14 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len);
 int unet_pack_weight(int dtype, const float* w_oihw, void* packed, int Cout, int Cin, int ksize,
                      int transpose, void* stream);
 int unet_packed_weight_elems(int dtype, int Cout, int Cin, int ksize, int transpose);
+/* many weights in one launch (all convs of a network forward, or all dgrad packs of a backward) */
+#define UNET_PACK_MAX_JOBS 64
+typedef struct unet_pack_job {
+  const float* w;         /* OIHW fp32                                                            */
+  void* packed;           /* unet_packed_weight_elems(dtype, Cout, Cin, ksize, transpose) elements   */
+  int Cout, Cin, ksize, transpose;
+} unet_pack_job;
+int unet_pack_weights(int dtype, int count, const unet_pack_job* jobs, void* stream);
 
 /* ---- convolution (fwd / dgrad) ------------------------------------------------------------- */
 /* replaces nn.Conv2d.forward (3x3 pad1 / 1x1, no bias) on a transformed input — layers.py:31-38,
@@ -209,6 +217,9 @@ int unet_nhwc_to_nchw(int dtype, long long N, int C, int H, int W, const void* x
 int unet_gated_to_nchw(int dtype, long long N, int C, int H, int W, const void* x, const float* scale,
                        const float* shift, int relu, const float* p, const float* psi_ab, float* y, void* stream);
 int unet_fill_f32(float* x, long long n, float v, void* stream);
+/* write the virtual source `src` (as a conv with an N x H x W input would read it: pool, bilinear-up
+ * + pad, BN-apply/ReLU, attention gate) as a plain NHWC tensor of op dtype [N,H,W,src->C]          */
+int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, void* out, void* stream);
 
 /* ---- DiceBCE / Dice / BalancedCE loss + grad — loss.py:18-191 ------------------------------- */
 int unet_loss_rows(long long HW);

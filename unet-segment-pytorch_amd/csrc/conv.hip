@@ -417,6 +417,43 @@ __global__ void pack_kernel(const float* w, T* out, int Cout, int Cin, int ks, i
   }
 }
 
+// many weights in one launch: job table passed by value in the kernel arguments; blockIdx.y = job
+struct PackJobs {
+  unet_pack_job j[UNET_PACK_MAX_JOBS];
+};
+
+template <typename T>
+__global__ void pack_many_kernel(const PackJobs jobs) {
+  const unet_pack_job& jb = jobs.j[blockIdx.y];
+  constexpr int KC = Mma<T>::KC, E16 = 16 / (int)sizeof(T);
+  const int taps = jb.ksize * jb.ksize;
+  const int rows = jb.transpose ? jb.Cin : jb.Cout;
+  const int cols = jb.transpose ? jb.Cout : jb.Cin;
+  const int rows_pad = (rows + PACK_NPAD - 1) / PACK_NPAD * PACK_NPAD;
+  const int nchunks = (cols + KC - 1) / KC;
+  const long long total = (long long)rows_pad * nchunks * KC * taps;
+  T* out = (T*)jb.packed;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int el = e % E16;
+    long long t = e / E16;
+    const int lane = t % 64;
+    t /= 64;
+    const int tap = t % taps;
+    t /= taps;
+    const int chunk = t % nchunks;
+    const int ntile = t / nchunks;
+    const int r = ntile * 16 + (lane & 15);
+    const int k = (sizeof(T) == 2) ? 8 * (lane >> 4) + el : 4 * el + (lane >> 4);
+    const int cc = chunk * KC + k;
+    float v = 0.f;
+    if (r < rows && cc < cols) {
+      if (!jb.transpose) v = jb.w[((long long)r * jb.Cin + cc) * taps + tap];
+      else v = jb.w[((long long)cc * jb.Cin + r) * taps + (taps - 1 - tap)];
+    }
+    out[e] = from_f<T>(v);
+  }
+}
+
 static int packed_rows(int Cout, int Cin, int transpose) {
   return round_up(transpose ? Cin : Cout, PACK_NPAD);
 }
@@ -457,6 +494,34 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
   snprintf(buf, len, "conv2_kernel<%s,%d,%d,%d,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize, c.wm, c.wn,
            c.ntn, c.raw);
   return 0;
+}
+
+int unet_pack_weights(int dtype, int count, const unet_pack_job* jobs, void* stream) {
+  if (count < 0 || count > UNET_PACK_MAX_JOBS || (count && !jobs)) {
+    set_error("unet_pack_weights: bad job count");
+    return UNET_ERR_ARG;
+  }
+  if (count == 0) return 0;
+  PackJobs pj;
+  long long maxe = 0;
+  for (int i = 0; i < count; ++i) {
+    pj.j[i] = jobs[i];
+    const unet_pack_job& j = jobs[i];
+    if (!j.w || !j.packed || j.Cout <= 0 || j.Cin <= 0 || (j.ksize != 1 && j.ksize != 3)) {
+      set_error("unet_pack_weights: bad job");
+      return UNET_ERR_ARG;
+    }
+    const long long e = unet_packed_weight_elems(dtype, j.Cout, j.Cin, j.ksize, j.transpose);
+    if (e > maxe) maxe = e;
+  }
+  int blocks = (int)((maxe + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(pack_many_kernel<bf16>, dim3(blocks, count), dim3(256), 0, st, pj);
+  else
+    hipLaunchKernelGGL(pack_many_kernel<float>, dim3(blocks, count), dim3(256), 0, st, pj);
+  return check_launch("pack_weights");
 }
 
 int unet_packed_weight_elems(int dtype, int Cout, int Cin, int ksize, int transpose) {

@@ -1,5 +1,5 @@
 // misc.hip — bilinear adjoint, NCHW resize (deep-supervision heads), OutConv, layout, fill.
-#include "src_gather.h"
+#include "halo_items.h"
 
 namespace unet {
 
@@ -320,6 +320,34 @@ __global__ void nchw_to_nhwc_kernel(long long N, int C, int H, int W, const floa
     y[e] = from_f<T>(x[(n * C + c) * (long long)H * W + hw]);
   }
 }
+// ---- materialise a virtual source (max-pool / bilinear-up + pad / BN-ReLU / gate) as a plain NHWC
+// tensor.  The conv and wgrad loaders then read it as a PLAIN source: their per-element transform
+// (VALU beside the MFMAs) costs more than one streaming pass over the result.
+template <typename T>
+__global__ void materialize_kernel(const unet_src s, long long N, int H, int W, T* out) {
+  constexpr int VEC = Vec<T>::N;
+  const int CV = (s.C + VEC - 1) / VEC;
+  const long long total = N * H * (long long)W * CV;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int cv = (int)(e % CV);
+    long long t = e / CV;
+    const int x = (int)(t % W);
+    t /= W;
+    const int y = (int)(t % H);
+    const long long n = t / H;
+    float v[VEC];
+    src_gather<T>(&s, 1, s.C, H, W, n, y, x, cv * VEC, v);
+    T* o = out + ((n * H + y) * (long long)W + x) * s.C + cv * VEC;
+    if ((s.C % VEC) == 0) {
+      store_vec<T>(o, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (cv * VEC + j < s.C) o[j] = from_f<T>(v[j]);
+    }
+  }
+}
+
 template <typename T>
 __global__ void nhwc_to_nchw_kernel(long long N, int C, int H, int W, const T* x, const float* sc, const float* sf,
                                     int relu, float* y) {
@@ -425,6 +453,41 @@ static inline int oc_rows(long long P) {
   if (r > 1024) r = 1024;
   if (r < 1) r = 1;
   return (int)r;
+}
+
+// fast form (C % VEC == 0): e = pixel * CV + cv with cv fastest, so stores are coalesced and, since
+// the grid stride is a multiple of CV (a power of two <= 256 here), every thread keeps one channel
+// vector: its BN scale/shift are loaded once (make_view) and each pixel is one item_issue/finish
+struct MatDesc {
+  int nsrc;
+  unet_src src[2];
+  int Cin;
+};
+
+template <typename T, int RAW>
+__global__ void materialize_fast_kernel(const MatDesc d, long long N, int H, int W, T* out) {
+  constexpr int VEC = Vec<T>::N;
+  const int C = d.src[0].C;
+  const int CV = C / VEC;
+  const long long total = N * H * (long long)W * CV;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const int cv = (int)(e % CV);
+  SrcView sv;
+  float sc[VEC], sf[VEC];
+  make_view<T>(d, cv * VEC, sv, sc, sf);
+  for (; e < total; e += stride) {
+    const long long px = e / CV;
+    const int x = (int)(px % W);
+    const long long t = px / W;
+    const int y = (int)(t % H);
+    const int n = (int)(t / H);
+    Item<RAW> it;
+    item_issue<T, RAW>(sv, H, W, n, y, x, 1, it);
+    float v[VEC];
+    item_finish<T, RAW>(d, sv, sc, sf, n, y, x, cv * VEC, it, v);
+    store_vec<T>(out + px * C + cv * VEC, v);
+  }
 }
 
 }  // namespace unet
@@ -565,6 +628,44 @@ int unet_convt_bwd_prep(int dtype, long long N, int h, int w, int Ct, int Hp, in
     hipLaunchKernelGGL(convt_bwd_prep_kernel<float>, dim3(rows), dim3(256), 0, st, N, h, w, Ct, Hp, Wp, pad_t, pad_l,
                        d_up, (float*)dy_s2d, partial, rows);
   return check_launch("convt_bwd_prep");
+}
+
+int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, void* out, void* stream) {
+  if (!src || !out || N <= 0 || H <= 0 || W <= 0 || src->C <= 0 || !src->data || src->kind == UNET_SRC_NCHW_F32) {
+    set_error("unet_materialize: bad arguments");
+    return UNET_ERR_ARG;
+  }
+  const int vec = dtype == UNET_BF16 ? 8 : 4;
+  const long long total = N * H * (long long)W * ((src->C + vec - 1) / vec);
+  long long b = (total + 255) / 256;
+  if (b > 16384) b = 16384;
+  const int cv = src->C / vec;
+  // 32-bit gather offsets in item_issue: the source must stay below 4 GiB
+  const double bytes = (double)N * src->H * src->W * src->C * (dtype == UNET_BF16 ? 2 : 4);
+  if (src->C % vec == 0 && cv <= 256 && (cv & (cv - 1)) == 0 && bytes < 4294967296.0) {
+    MatDesc md;
+    md.nsrc = 1;
+    md.src[0] = *src;
+    md.src[1] = *src;
+    md.Cin = src->C;
+    const int raw = (src->kind == UNET_SRC_POOL_ACT || src->kind == UNET_SRC_UP_ACT) ? 4 : 1;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == UNET_BF16) {
+      if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<bf16, 4>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (bf16*)out);
+      else hipLaunchKernelGGL((materialize_fast_kernel<bf16, 1>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (bf16*)out);
+    } else {
+      if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<float, 4>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (float*)out);
+      else hipLaunchKernelGGL((materialize_fast_kernel<float, 1>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (float*)out);
+    }
+    return check_launch("materialize");
+  }
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(materialize_kernel<bf16>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, *src, N, H, W,
+                       (bf16*)out);
+  else
+    hipLaunchKernelGGL(materialize_kernel<float>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, *src, N, H, W,
+                       (float*)out);
+  return check_launch("materialize");
 }
 
 int unet_fill_f32(float* x, long long n, float v, void* stream) {

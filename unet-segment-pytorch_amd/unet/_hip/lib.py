@@ -34,6 +34,13 @@ class ConvDesc(ctypes.Structure):
                 ("stats", c_vp), ("pool_src", Src), ("bias", c_vp)]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("w", c_vp), ("packed", c_vp), ("Cout", c_int), ("Cin", c_int), ("ksize", c_int), ("transpose", c_int)]
+
+
+PACK_MAX_JOBS = 64
+
+
 class WgradDesc(ctypes.Structure):
     _fields_ = [("dtype", c_int), ("N", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
                 ("ksize", c_int), ("nsrc", c_int), ("src", Src * 2), ("dy", c_vp), ("dw", c_vp), ("accum", c_int),
@@ -49,6 +56,7 @@ _SIGS = {
     "unet_conv_variant": (c_int, [ctypes.POINTER(ConvDesc), ctypes.c_char_p, c_int]),
     "unet_pack_weight": (c_int, [c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "unet_packed_weight_elems": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "unet_pack_weights": (c_int, [c_int, c_int, ctypes.POINTER(PackJob), c_vp]),
     "unet_conv": (c_int, [ctypes.POINTER(ConvDesc), c_vp]),
     "unet_wgrad_workspace": (c_size, [ctypes.POINTER(WgradDesc)]),
     "unet_conv_wgrad": (c_int, [ctypes.POINTER(WgradDesc), c_vp]),
@@ -86,6 +94,7 @@ _SIGS = {
     "unet_nhwc_to_nchw": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "unet_gated_to_nchw": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "unet_fill_f32": (c_int, [c_vp, c_ll, c_float, c_vp]),
+    "unet_materialize": (c_int, [c_int, ctypes.POINTER(Src), c_ll, c_int, c_int, c_vp, c_vp]),
     "unet_loss_rows": (c_int, [c_ll]),
     "unet_loss_reduce": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp]),
     "unet_loss_finalize": (c_int, [c_vp, c_int, c_ll, c_int, c_float, c_float, c_float, c_float, c_float, c_int, c_int,

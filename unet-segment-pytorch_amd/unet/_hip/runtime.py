@@ -139,6 +139,30 @@ def pack_weight(w: torch.Tensor, prec: Precision, transpose: bool) -> torch.Tens
     return out
 
 
+def pack_many(items, prec: Precision):
+    """Pack several OIHW weights (list of (weight, transpose)) with one launch per 64; returns the
+    packed tensors in order."""
+    lib = L.load()
+    outs, jobs, keep = [], [], []
+    for w, transpose in items:
+        cout, cin, k = w.shape[0], w.shape[1], w.shape[2]
+        n = lib.unet_packed_weight_elems(prec.code, cout, cin, k, int(transpose))
+        out = torch.empty(n, dtype=prec.torch_dtype, device=w.device)
+        wc = w.detach()
+        if wc.dtype != torch.float32 or not wc.is_contiguous():
+            wc = wc.float().contiguous()
+        keep.append(wc)
+        j = L.PackJob()
+        j.w, j.packed, j.Cout, j.Cin, j.ksize, j.transpose = wc.data_ptr(), out.data_ptr(), cout, cin, k, int(transpose)
+        jobs.append(j)
+        outs.append(out)
+    for i in range(0, len(jobs), L.PACK_MAX_JOBS):
+        chunk = jobs[i:i + L.PACK_MAX_JOBS]
+        arr = (L.PackJob * len(chunk))(*chunk)
+        L.call("unet_pack_weights", prec.code, len(chunk), arr, stream())
+    return outs
+
+
 def fill_zero(t: torch.Tensor) -> None:
     L.call("unet_fill_f32", vp(t), t.numel(), 0.0, stream())
 

@@ -13,7 +13,7 @@ from typing import Dict, List, Optional
 import torch
 
 from . import lib as L
-from .runtime import (Act, Precision, conv_kernel_name, f32, pack_weight, probe, stream, up_scale, vp,
+from .runtime import (Act, Precision, conv_kernel_name, f32, pack_many, pack_weight, probe, stream, up_scale, vp,
                       wgrad_kernel_name)
 
 
@@ -27,6 +27,13 @@ def _conv_desc(prec: Precision, N: int, H: int, W: int, cin: int, cout: int, k: 
         d.src[i] = s
     d.weight = weight.data_ptr()
     return d
+
+
+def _materialize(prec: Precision, src: L.Src, N: int, H: int, W: int) -> torch.Tensor:
+    """The virtual source as a plain NHWC tensor (what the consuming conv's loader would have built)."""
+    out = torch.empty(N, H, W, src.C, dtype=prec.torch_dtype, device="cuda")
+    L.call("unet_materialize", prec.code, src, N, H, W, vp(out), stream())
+    return out
 
 
 def _plain_src(t: torch.Tensor) -> L.Src:
@@ -56,12 +63,15 @@ class ConvBN:
         self.conv, self.bn, self.relu = conv, bn, relu
         self.k = conv.kernel_size[0]
         self.cin, self.cout = conv.in_channels, conv.out_channels
+        self.pre_wp = None   # packed forward / dgrad weights, set by NetworkPlan's batched pack
+        self.pre_wt = None
 
     # ---- forward ----
     def forward(self, prec: Precision, srcs: List[L.Src], N: int, H: int, W: int, training: bool,
                 keep=None) -> Act:
         dev = self.conv.weight.device
-        wp = pack_weight(self.conv.weight, prec, transpose=False)
+        wp = self.pre_wp if self.pre_wp is not None else pack_weight(self.conv.weight, prec, transpose=False)
+        self.pre_wp = None
         y = torch.empty(N, H, W, self.cout, dtype=prec.torch_dtype, device=dev)
         d = _conv_desc(prec, N, H, W, self.cin, self.cout, self.k, srcs, wp)
         d.out_mode = L.OUT_Y
@@ -137,7 +147,8 @@ class ConvBN:
         grads.put(self.conv.weight, dw)
         if dgrad is None:
             return
-        wt = pack_weight(self.conv.weight, prec, transpose=True)
+        wt = self.pre_wt if self.pre_wt is not None else pack_weight(self.conv.weight, prec, transpose=True)
+        self.pre_wt = None
         d = _conv_desc(prec, N, H, W, self.cout, self.cin, self.k, [_plain_src(dy)], wt)
         if dgrad["mode"] == "pool":
             d.out_mode = L.OUT_POOL_BWD
@@ -190,11 +201,12 @@ class GateStage:
         self.psi_conv, self.psi_bn = m.psi[0], m.psi[1]
         self.ci = self.cg.cout
 
-    def forward(self, prec, g: Act, x: Act, training: bool):
+    def forward(self, prec, g: Act, x: Act, training: bool, g_up: Optional[L.Src] = None):
         N, H, W = x.N, x.H, x.W
         dev = x.data.device
         self.g, self.x = g, x
-        self.src_g = g.src_up(H, W, 0, 0)
+        # bilinear(g -> x size) (layers.py:183): the Up stage's materialised map when it is the same one
+        self.src_g = g_up if g_up is not None else g.src_up(H, W, 0, 0)
         self.gw = self.cg.forward(prec, [self.src_g], N, H, W, training)
         self.gw_src = [self.src_g]
         self.xw = self.cx.forward(prec, [x.src()], N, H, W, training)
@@ -378,8 +390,14 @@ class UpStage:
         self.x1, self.x2 = x1, x2
         self.geo = _pad_geometry(x1, x2)
         up_h, up_w, pt, pl = self.geo
+        up_t = None
+        if self.convt is None:
+            # bilinear x2 of relu(bn(x1)), padded into the skip's frame, written once (layers.py:78,98-102)
+            up_t = _materialize(prec, x1.src_up(up_h, up_w, pt, pl), x2.N, x2.H, x2.W)
+            self.up_t = up_t
         if self.gate is not None:
-            self.gate.forward(prec, x1, x2, training)
+            same = up_t is not None and up_h == x2.H and up_w == x2.W and pt == 0 and pl == 0
+            self.gate.forward(prec, x1, x2, training, g_up=_plain_src(up_t) if same else None)
             skip = self.gate.gated_src()
         else:
             skip = x2.src()
@@ -387,7 +405,7 @@ class UpStage:
             self.u = self.convt.forward(prec, x1)
             up = self.u.src_placed(pt, pl)
         else:
-            up = x1.src_up(up_h, up_w, pt, pl)
+            up = _plain_src(up_t)
         return self.dc.forward(prec, [skip, up], x2.N, x2.H, x2.W, training)
 
     def backward(self, prec, grads: Grads):
@@ -429,7 +447,9 @@ class DownStage:
 
     def forward(self, prec, x: Act, training: bool) -> Act:
         self.x = x
-        return self.dc.forward(prec, [x.src_pool()], x.N, x.H // 2, x.W // 2, training)
+        # MaxPool2d(2)(relu(bn(y))) written once (quarter size); the conv, its wgrad read it plain
+        self.xp = _materialize(prec, x.src_pool(), x.N, x.H // 2, x.W // 2)
+        return self.dc.forward(prec, [_plain_src(self.xp)], x.N, x.H // 2, x.W // 2, training)
 
     def backward(self, prec, grads: Grads):
         g = self.x.grad_zeroed()
@@ -509,10 +529,24 @@ class NetworkPlan:
         if self.ds:
             self.heads = [DSHeadStage(model.ds_out1), DSHeadStage(model.ds_out2), DSHeadStage(model.ds_out3)]
 
+    def convbns(self):
+        """Every conv -> BN pair of the network (their weights are packed in one launch)."""
+        out = [self.inc.c1, self.inc.c2]
+        for d in self.downs:
+            out += [d.dc.c1, d.dc.c2]
+        for u in self.ups:
+            out += [u.dc.c1, u.dc.c2]
+            if u.gate is not None:
+                out += [u.gate.cg, u.gate.cx]
+        return out
+
     def forward(self, prec: Precision, x: torch.Tensor, training: bool, need_dx: bool):
         N, C, H, W = x.shape
         self.x = x
         self.need_dx = need_dx
+        cbs = self.convbns()
+        for cb, wp in zip(cbs, pack_many([(cb.conv.weight, False) for cb in cbs], prec)):
+            cb.pre_wp = wp
         xs = [self.inc.forward(prec, [_nchw(x)], N, H, W, training, keep=x)]
         for d in self.downs:
             xs.append(d.forward(prec, xs[-1], training))
@@ -534,6 +568,9 @@ class NetworkPlan:
         return [logits]
 
     def backward(self, prec: Precision, gouts, grads: Grads):
+        cbs = [cb for cb in self.convbns() if cb is not self.inc.c1 or self.need_dx]
+        for cb, wt in zip(cbs, pack_many([(cb.conv.weight, True) for cb in cbs], prec)):
+            cb.pre_wt = wt
         gl = gouts[0]
         if gl is None:
             gl = torch.zeros(self.x.shape[0], self.outc.k, self.x.shape[2], self.x.shape[3], device=self.x.device)
