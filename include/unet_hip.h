@@ -82,6 +82,8 @@ typedef struct unet_conv_desc {
   float* stats;           /* Y: [2][mtiles][Cout] partial sum / sum of squares (may be NULL)       */
   unet_src pool_src;      /* POOL_BWD: the pre-pool activation (kind ACT, H=2H', W=2W')           */
   const float* bias;      /* SHUFFLE2: fp32 [Ct] (may be NULL)                                     */
+  const uint8_t* pool_code; /* POOL_BWD, optional: 2x2 argmax (0..3, row-major) per pooled element and
+                             channel [N,H,W,Cout], as written by unet_materialize_pool             */
 } unet_conv_desc;
 
 typedef struct unet_wgrad_desc {
@@ -220,6 +222,10 @@ int unet_fill_f32(float* x, long long n, float v, void* stream);
 /* write the virtual source `src` (as a conv with an N x H x W input would read it: pool, bilinear-up
  * + pad, BN-apply/ReLU, attention gate) as a plain NHWC tensor of op dtype [N,H,W,src->C]          */
 int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, void* out, void* stream);
+/* MaxPool2d(2) of an ACT source (kind POOL_ACT) as a plain tensor plus its argmax codes (0..3 in
+ * the window's row-major order, first maximum wins as in ATen; uint8 [N,H,W,C]) — layers.py:56   */
+int unet_materialize_pool(int dtype, const unet_src* src, long long N, int H, int W, void* out, uint8_t* code,
+                          void* stream);
 
 /* ---- DiceBCE / Dice / BalancedCE loss + grad — loss.py:18-191 ------------------------------- */
 int unet_loss_rows(long long HW);

@@ -123,6 +123,26 @@ __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&a
         }
       }
     }
+  } else if (d.pool_code) {  // UNET_OUT_POOL_BWD with the argmax recorded by unet_materialize_pool
+    const unet_src& ps = d.pool_src;
+    float* da = (float*)d.out;
+#pragma unroll MI
+    for (int i = 0; i < MI; ++i) {
+      const int oh = h0 + wm * MI + i;
+#pragma unroll NTN
+      for (int j = 0; j < NTN; ++j) {
+        const int co = co0 + (wn * NTN + j) * 16 + (lane & 15);
+#pragma unroll 4
+        for (int r = 0; r < 4; ++r) {
+          const int ow = ow_base + r;
+          if (oh < d.H && ow < d.W && co < d.Cout) {
+            const int bq = d.pool_code[((n * d.H + oh) * (long long)d.W + ow) * d.Cout + co];
+            const long long sp = (n * ps.H + 2 * oh + (bq >> 1)) * (long long)ps.W + 2 * ow + (bq & 1);
+            da[sp * d.Cout + co] += acc[i][j][r];
+          }
+        }
+      }
+    }
   } else {  // UNET_OUT_POOL_BWD
     const unet_src& ps = d.pool_src;
     float* da = (float*)d.out;

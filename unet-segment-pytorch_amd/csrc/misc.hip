@@ -490,6 +490,51 @@ __global__ void materialize_fast_kernel(const MatDesc d, long long N, int H, int
   }
 }
 
+// MaxPool2d(2) of relu?(scale*y + shift) with argmax codes; one thread per pooled channel vector
+template <typename T>
+__global__ void materialize_pool_kernel(const unet_src s, long long N, int H, int W, T* out, uint8_t* code) {
+  constexpr int VEC = Vec<T>::N;
+  const int C = s.C, CV = C / VEC;
+  const long long total = N * H * (long long)W * CV;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const int cv = (int)(e % CV);
+  float sc[VEC], sf[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) { sc[j] = s.scale[cv * VEC + j]; sf[j] = s.shift[cv * VEC + j]; }
+  const float lo = s.relu ? 0.f : -INFINITY;
+  for (; e < total; e += stride) {
+    const long long px = e / CV;
+    const int x = (int)(px % W);
+    const long long t = px / W;
+    const int y = (int)(t % H);
+    const long long n = t / H;
+    float best[VEC];
+    int arg[VEC];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v[VEC];
+      load_vec<T>((const T*)s.data + (((n * s.H + 2 * y + (q >> 1)) * (long long)s.W + 2 * x + (q & 1)) * C + cv * VEC), v);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float a = fmaxf(v[j] * sc[j] + sf[j], lo);
+        if (q == 0 || a > best[j] || a != a) { best[j] = a; arg[j] = q; }
+      }
+    }
+    store_vec<T>(out + px * C + cv * VEC, best);
+    unsigned lo4 = 0, hi4 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo4 |= (unsigned)arg[j] << (8 * j);
+    if constexpr (VEC == 8) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hi4 |= (unsigned)arg[4 + j] << (8 * j);
+      *reinterpret_cast<uint2*>(code + px * C + cv * VEC) = make_uint2(lo4, hi4);
+    } else {
+      *reinterpret_cast<unsigned*>(code + px * C + cv * VEC) = lo4;
+    }
+  }
+}
+
 }  // namespace unet
 
 using namespace unet;
@@ -666,6 +711,26 @@ int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, 
     hipLaunchKernelGGL(materialize_kernel<float>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, *src, N, H, W,
                        (float*)out);
   return check_launch("materialize");
+}
+
+int unet_materialize_pool(int dtype, const unet_src* src, long long N, int H, int W, void* out, uint8_t* code,
+                          void* stream) {
+  const int vec = dtype == UNET_BF16 ? 8 : 4;
+  const int cv = src ? src->C / vec : 0;
+  if (!src || !out || !code || src->kind != UNET_SRC_POOL_ACT || !src->scale || !src->shift || src->C % vec ||
+      cv > 256 || (cv & (cv - 1)) || src->H < 2 * H || src->W < 2 * W) {
+    set_error("unet_materialize_pool: needs a POOL_ACT source with C/vec a power of two <= 256");
+    return UNET_ERR_ARG;
+  }
+  const long long total = N * H * (long long)W * cv;
+  long long b = (total + 255) / 256;
+  if (b > 16384) b = 16384;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == UNET_BF16)
+    hipLaunchKernelGGL(materialize_pool_kernel<bf16>, dim3((int)b), dim3(256), 0, st, *src, N, H, W, (bf16*)out, code);
+  else
+    hipLaunchKernelGGL(materialize_pool_kernel<float>, dim3((int)b), dim3(256), 0, st, *src, N, H, W, (float*)out, code);
+  return check_launch("materialize_pool");
 }
 
 int unet_fill_f32(float* x, long long n, float v, void* stream) {

@@ -31,7 +31,7 @@ class ConvDesc(ctypes.Structure):
     _fields_ = [("dtype", c_int), ("N", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
                 ("ksize", c_int), ("nsrc", c_int), ("src", Src * 2), ("weight", c_vp), ("out_mode", c_int),
                 ("out", c_vp), ("out2", c_vp), ("split", c_int), ("accum", c_int), ("accum2", c_int),
-                ("stats", c_vp), ("pool_src", Src), ("bias", c_vp)]
+                ("stats", c_vp), ("pool_src", Src), ("bias", c_vp), ("pool_code", c_vp)]
 
 
 class PackJob(ctypes.Structure):
@@ -95,6 +95,7 @@ _SIGS = {
     "unet_gated_to_nchw": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "unet_fill_f32": (c_int, [c_vp, c_ll, c_float, c_vp]),
     "unet_materialize": (c_int, [c_int, ctypes.POINTER(Src), c_ll, c_int, c_int, c_vp, c_vp]),
+    "unet_materialize_pool": (c_int, [c_int, ctypes.POINTER(Src), c_ll, c_int, c_int, c_vp, c_vp, c_vp]),
     "unet_loss_rows": (c_int, [c_ll]),
     "unet_loss_reduce": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp]),
     "unet_loss_finalize": (c_int, [c_vp, c_int, c_ll, c_int, c_float, c_float, c_float, c_float, c_float, c_int, c_int,

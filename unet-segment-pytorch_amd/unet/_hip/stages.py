@@ -154,6 +154,7 @@ class ConvBN:
             d.out_mode = L.OUT_POOL_BWD
             d.out = dgrad["out"].data_ptr()
             d.pool_src = dgrad["pool_src"]
+            d.pool_code = vp(dgrad.get("code"))
         else:
             d.out_mode = L.OUT_F32
             d.out = dgrad["out"].data_ptr()
@@ -448,12 +449,22 @@ class DownStage:
     def forward(self, prec, x: Act, training: bool) -> Act:
         self.x = x
         # MaxPool2d(2)(relu(bn(y))) written once (quarter size); the conv, its wgrad read it plain
-        self.xp = _materialize(prec, x.src_pool(), x.N, x.H // 2, x.W // 2)
-        return self.dc.forward(prec, [_plain_src(self.xp)], x.N, x.H // 2, x.W // 2, training)
+        h, w = x.H // 2, x.W // 2
+        self.xp = torch.empty(x.N, h, w, x.C, dtype=prec.torch_dtype, device=x.data.device)
+        self.code = None
+        vec = 8 if prec.code == L.BF16 else 4
+        cv = x.C // vec
+        if x.C % vec == 0 and cv <= 256 and cv & (cv - 1) == 0:
+            # the 2x2 argmax is recorded too: the pool backward then routes by one byte per element
+            self.code = torch.empty(x.N, h, w, x.C, dtype=torch.uint8, device=x.data.device)
+            L.call("unet_materialize_pool", prec.code, x.src_pool(), x.N, h, w, vp(self.xp), vp(self.code), stream())
+        else:
+            L.call("unet_materialize", prec.code, x.src_pool(), x.N, h, w, vp(self.xp), stream())
+        return self.dc.forward(prec, [_plain_src(self.xp)], x.N, h, w, training)
 
     def backward(self, prec, grads: Grads):
         g = self.x.grad_zeroed()
-        self.dc.backward(prec, grads, {"mode": "pool", "out": g, "pool_src": self.x.src_pool()})
+        self.dc.backward(prec, grads, {"mode": "pool", "out": g, "pool_src": self.x.src_pool(), "code": self.code})
 
 
 class OutConvStage:
