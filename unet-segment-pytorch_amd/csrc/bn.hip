@@ -120,6 +120,104 @@ __global__ void bn_bwd_reduce_kernel(long long P, int C, int CL, const float* da
   }
 }
 
+// vectorised forms (C % 8 == 0): a thread owns 8 channels (16-byte y, 2 x 16-byte da) of one pixel;
+// the block covers 256 / (C/8) pixels per iteration with a fixed channel vector per thread
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int C, const float* da, const T* y,
+                                                                const float* scale, const float* shift, int relu,
+                                                                const float* mean, const float* invstd, float* part,
+                                                                int rows) {
+  __shared__ float sh[2][256 * 8 / 8];
+  const int CV = C / 8, tid = threadIdx.x;
+  const int cv = tid % CV, py = tid / CV, R = 256 / CV;
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  float sc[8], sf[8], mu[8], is[8], sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cv * 8 + j;
+    sc[j] = scale[c]; sf[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
+    sg[j] = 0.f; sgx[j] = 0.f;
+  }
+  if (py < R) {
+    for (long long p = p0 + py; p < p1; p += R) {
+      float yv[8], g[8];
+      load_vec<T>(y + p * C + cv * 8, yv);
+      if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
+      load_vec<float>(da + p * C + cv * 8, g);
+      load_vec<float>(da + p * C + cv * 8 + 4, g + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[j];
+        sg[j] += gj;
+        sgx[j] += gj * (yv[j] - mu[j]) * is[j];
+      }
+    }
+  }
+  // reduce over the R pixel rows of each channel vector (fixed order)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[0][tid] = sg[j];
+    sh[1][tid] = sgx[j];
+    __syncthreads();
+    if (tid < CV) {
+      float a = 0.f, b = 0.f;
+      for (int r = 0; r < R; ++r) { a += sh[0][r * CV + tid]; b += sh[1][r * CV + tid]; }
+      part[(size_t)blockIdx.x * C + tid * 8 + j] = a;
+      part[((size_t)rows + blockIdx.x) * C + tid * 8 + j] = b;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int C, const float* da, const T* y,
+                                                               const float* scale, const float* shift, int relu,
+                                                               const float* coef, T* dy) {
+  const int CV = C / 8;
+  const long long total = P * CV;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const int cv = (int)(e % CV);  // fixed: the stride is a multiple of CV (power of two <= 256)
+  float sc[8], sf[8], A[8], B[8], Cc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cv * 8 + j;
+    sc[j] = scale[c]; sf[j] = shift[c]; A[j] = coef[c]; B[j] = coef[C + c]; Cc[j] = coef[2 * C + c];
+  }
+  for (; e < total; e += stride) {
+    const long long p = e / CV;
+    float yv[8], g[8], o[8];
+    load_vec<T>(y + p * C + cv * 8, yv);
+    if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
+    load_vec<float>(da + p * C + cv * 8, g);
+    load_vec<float>(da + p * C + cv * 8 + 4, g + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[j];
+      o[j] = A[j] * gj + B[j] * yv[j] + Cc[j];
+    }
+    if constexpr (sizeof(T) == 2) {
+      store_vec<T>(dy + p * C + cv * 8, o);
+    } else {
+      store_vec<T>(dy + p * C + cv * 8, o);
+      store_vec<T>(dy + p * C + cv * 8 + 4, o + 4);
+    }
+  }
+}
+
+static inline bool bn_vec_ok(int C) {
+  const int cv = C / 8;
+  return C % 8 == 0 && cv <= 256 && (cv & (cv - 1)) == 0;
+}
+static inline int reduce_rows_vec(long long P, int C) {
+  const int R = 256 / (C / 8);
+  long long r = (P + 8LL * R - 1) / (8LL * R);  // >= 8 pixel iterations per thread
+  if (r > 2048) r = 2048;
+  if (r < 1) r = 1;
+  return (int)r;
+}
+
 // one block per channel: sums over rows in fp64
 __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
                                        const float* gamma, const float* mean, const float* invstd, float* dgamma,
@@ -200,11 +298,21 @@ int unet_bn_eval_affine(int C, const float* gamma, const float* beta, const floa
   return check_launch("bn_eval_affine");
 }
 
-int unet_bn_bwd_reduce_rows(long long P, int C) { return reduce_rows(P, C); }
+int unet_bn_bwd_reduce_rows(long long P, int C) { return bn_vec_ok(C) ? reduce_rows_vec(P, C) : reduce_rows(P, C); }
 
 int unet_bn_bwd_reduce(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
                        const float* shift, int relu, const float* mean, const float* invstd, float* partial,
                        void* stream) {
+  if (bn_vec_ok(C)) {
+    const int rows = reduce_rows_vec(P, C);
+    if (dtype == UNET_BF16)
+      hipLaunchKernelGGL(bn_bwd_reduce_vec_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, C, da,
+                         (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
+    else
+      hipLaunchKernelGGL(bn_bwd_reduce_vec_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, C, da,
+                         (const float*)y, scale, shift, relu, mean, invstd, partial, rows);
+    return check_launch("bn_bwd_reduce");
+  }
   const int cl = chan_lanes(C), rows = reduce_rows(P, C);
   dim3 grid(cdiv(C, cl), rows);
   if (dtype == UNET_BF16)
@@ -226,6 +334,17 @@ int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int 
 
 int unet_bn_bwd_apply(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
                       const float* shift, int relu, const float* coef, void* dy, void* stream) {
+  if (bn_vec_ok(C)) {
+    long long b = (P * (C / 8) + 255) / 256;
+    if (b > 8192) b = 8192;
+    if (dtype == UNET_BF16)
+      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<bf16>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, P, C, da,
+                         (const bf16*)y, scale, shift, relu, coef, (bf16*)dy);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<float>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, P, C, da,
+                         (const float*)y, scale, shift, relu, coef, (float*)dy);
+    return check_launch("bn_bwd_apply");
+  }
   const int cl = chan_lanes(C), rows = reduce_rows(P, C);
   dim3 grid(cdiv(C, cl), rows);
   if (dtype == UNET_BF16)
