@@ -79,7 +79,7 @@ typedef struct unet_conv_desc {
   void* out2;             /* F32 split: fp32 [N,H,W,Cout-split]                                   */
   int split;              /* F32: channel split point (== Cout for no split)                       */
   int accum, accum2;      /* F32: add into out / out2 instead of storing                          */
-  float* stats;           /* Y: [2][mtiles][Cout] partial sum / sum of squares (may be NULL)       */
+  float* stats;           /* Y: [2][Cout][mtiles] partial sum / sum of squares (may be NULL)       */
   unet_src pool_src;      /* POOL_BWD: the pre-pool activation (kind ACT, H=2H', W=2W')           */
   const float* bias;      /* SHUFFLE2: fp32 [Ct] (may be NULL)                                     */
   const uint8_t* pool_code; /* POOL_BWD, optional: 2x2 argmax (0..3, row-major) per pooled element and
@@ -101,7 +101,7 @@ const char* unet_last_error(void);
 int unet_version(void);
 /* number of M tiles (8x16 output pixels) of a conv with this geometry: rows of the stats buffer  */
 int unet_conv_mtiles(int N, int H, int W);
-/* rows of the BN partial-sum buffer (stats = float[2][rows][Cout]) unet_conv will write for d    */
+/* rows of the BN partial-sum buffer (stats = float[2][Cout][rows]) unet_conv will write for d    */
 int unet_conv_stats_rows(const unet_conv_desc* d);
 /* name of the kernel instantiation unet_conv dispatches d to (for profiling / roofline probes)   */
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len);

@@ -220,7 +220,7 @@ def test_first_conv_nchw_input(prec, shape):
     d.dtype, d.N, d.H, d.W, d.Cin, d.Cout, d.ksize, d.nsrc = P.code, N, H, W, cin, cout, 3, 1
     d.src[0] = src
     rows = L.load().unet_conv_stats_rows(d)
-    st = torch.empty(2, rows, cout, device="cuda")
+    st = torch.empty(2, cout, rows, device="cuda")   # [2][Cout][rows] partial sums
     wp = R.pack_weight(w, P, transpose=False)
     d.weight, d.out_mode, d.out, d.stats = wp.data_ptr(), L.OUT_Y, out.data_ptr(), st.data_ptr()
     L.call("unet_conv", d, R.stream())
@@ -229,8 +229,8 @@ def test_first_conv_nchw_input(prec, shape):
     ref = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)
     tol = 1e-2 if prec == "bf16" else 1e-5
     assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max())
-    assert torch.allclose(st[0].sum(0), ref.sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
-    assert torch.allclose(st[1].sum(0), (ref * ref).sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(st[0].sum(1), ref.sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(st[1].sum(1), (ref * ref).sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
     # weight gradient
     dy = _rand(N, H, W, cout, dt=dt)
     refw = torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), dy.float().permute(0, 3, 1, 2), padding=1)

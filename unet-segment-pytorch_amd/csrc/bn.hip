@@ -36,8 +36,8 @@ __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long lon
   const int c = blockIdx.x;
   double s = 0, ss = 0;
   for (int r = threadIdx.x; r < rows; r += blockDim.x) {
-    s += stats[(size_t)r * C + c];
-    ss += stats[((size_t)rows + r) * C + c];
+    s += stats[(size_t)c * rows + r];           // [2][C][rows]: contiguous over r
+    ss += stats[((size_t)C + c) * rows + r];
   }
   s = block_sum_d(s, sh);
   ss = block_sum_d(ss, sh);

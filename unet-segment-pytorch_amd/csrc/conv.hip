@@ -77,8 +77,8 @@ __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&a
           float a = 0.f, b = 0.f;
 #pragma unroll
           for (int w = 0; w < WM; ++w) { a += red[(w * BN + tid) * 2]; b += red[(w * BN + tid) * 2 + 1]; }
-          d.stats[(size_t)mt * d.Cout + co] = a;
-          d.stats[((size_t)mtiles + mt) * d.Cout + co] = b;
+          d.stats[(size_t)co * mtiles + mt] = a;
+          d.stats[((size_t)d.Cout + co) * mtiles + mt] = b;
         }
       }
     }

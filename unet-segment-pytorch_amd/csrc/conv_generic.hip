@@ -131,8 +131,8 @@ __global__ __launch_bounds__(NTHR) void conv_generic_kernel(const unet_conv_desc
       if (tid < BN) {
         const int co = co0 + tid;
         if (co < d.Cout) {
-          d.stats[(size_t)mt * d.Cout + co] = red[tid * 2] + red[(BN + tid) * 2];
-          d.stats[((size_t)mtiles + mt) * d.Cout + co] = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
+          d.stats[(size_t)co * mtiles + mt] = red[tid * 2] + red[(BN + tid) * 2];
+          d.stats[((size_t)d.Cout + co) * mtiles + mt] = red[tid * 2 + 1] + red[(BN + tid) * 2 + 1];
         }
       }
     }

@@ -110,8 +110,8 @@ __global__ __launch_bounds__(256) void smallcin_fwd_kernel(const unet_conv_desc 
       float a = 0.f, b = 0.f;
       for (int q = 0; q < PPB; ++q) { a += red[0][q * G + tid]; b += red[1][q * G + tid]; }
       const int co = tid * 8 + j;
-      d.stats[(size_t)blockIdx.x * d.Cout + co] = a;
-      d.stats[((size_t)rows + blockIdx.x) * d.Cout + co] = b;
+      d.stats[(size_t)co * rows + blockIdx.x] = a;
+      d.stats[((size_t)d.Cout + co) * rows + blockIdx.x] = b;
     }
     __syncthreads();
   }

@@ -81,7 +81,7 @@ class ConvBN:
         use_batch = training or not bn.track_running_stats
         if use_batch:
             mt = L.load().unet_conv_stats_rows(d)
-            stats = f32(2, mt, self.cout, device=dev)
+            stats = f32(2, self.cout, mt, device=dev)   # [2][C][rows] (unet_conv_stats_rows)
             d.stats = stats.data_ptr()
         probe.launch(lambda: conv_kernel_name(d), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
                      lambda: L.call("unet_conv", d, stream()))
