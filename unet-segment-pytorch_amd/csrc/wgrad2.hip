@@ -271,7 +271,8 @@ W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   // wave tile = (16*MI co) x 16 ci x k*k taps.  3x3, Cout > 64: 8 waves of 32co (2 per SIMD, so one
   // wave's staging VALU runs beside the other's MFMAs; 72 accumulators fit the 256-VGPR budget)
   // (RAW=4 sources keep 4 waves: their staging registers do not fit beside 72 accumulators at 2/SIMD)
-  if (d->Cout <= 64) { p.wco = 1; p.wci = 4; p.mi = 4; }
+  if (d->Cout <= 64 && d->ksize == 3 && p.raw == 1) { p.wco = 2; p.wci = 4; p.mi = 2; }
+  else if (d->Cout <= 64) { p.wco = 1; p.wci = 4; p.mi = 4; }
   else if (d->ksize == 3 && p.raw == 1) { p.wco = 4; p.wci = 2; p.mi = 2; }
   else if (d->Cin >= 64) { p.wco = 2; p.wci = 4; p.mi = 4; }
   else { p.wco = 2; p.wci = 2; p.mi = 4; }
@@ -307,6 +308,7 @@ static int launch_w2_cfg(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t 
   if (p.wco == 1) return launch_w2<KS, 1, 4, 4, RAW>(d, p, st);
   if constexpr (KS == 3 && RAW == 1) {
     if (p.wco == 4) return launch_w2<KS, 4, 2, 2, RAW>(d, p, st);
+    if (p.wco == 2 && p.mi == 2) return launch_w2<KS, 2, 4, 2, RAW>(d, p, st);
   }
   if constexpr (KS == 1) {
     if (p.wci == 4) return launch_w2<KS, 2, 4, 4, RAW>(d, p, st);
