@@ -82,6 +82,43 @@ __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&a
         }
       }
     }
+  } else if (d.out_mode == UNET_OUT_F32 && (d.Cout % 4) == 0 && (d.split % 4) == 0) {
+    // fp32 gradients: each row of the wave's tile is transposed through a wave-private LDS slice so a
+    // lane stores (or read-modify-writes) 4 consecutive channels of one pixel as one 16-byte access,
+    // instead of 4-byte accesses strided by the pixel pitch
+    float* o1 = (float*)d.out;
+    float* o2 = (float*)d.out2;
+    const int c2 = d.Cout - d.split;
+    constexpr int SW = NTN * 16 + 4;  // staged row pitch in floats (the +4 keeps the writes conflict-free)
+    float* stg = reinterpret_cast<float*>(lds) + (wm * WN + wn) * 16 * SW;
+#pragma unroll MI
+    for (int i = 0; i < MI; ++i) {
+      const int oh = h0 + wm * MI + i;
+#pragma unroll NTN
+      for (int j = 0; j < NTN; ++j)
+#pragma unroll 4
+        for (int r = 0; r < 4; ++r) stg[(4 * (lane >> 4) + r) * SW + j * 16 + (lane & 15)] = acc[i][j][r];
+#pragma unroll
+      for (int k = 0; k < NTN; ++k) {
+        const int f = lane + 64 * k;
+        const int px = f / (4 * NTN), c4 = f % (4 * NTN);
+        const float4 v = *reinterpret_cast<const float4*>(stg + px * SW + c4 * 4);
+        const int ow = w0 + px, co = co0 + wn * NTN * 16 + c4 * 4;
+        if (oh < d.H && ow < d.W && co < d.Cout) {
+          const long long pix = (n * d.H + oh) * (long long)d.W + ow;
+          float4* p;
+          int acc_in;
+          if (co < d.split) { p = reinterpret_cast<float4*>(o1 + pix * d.split + co); acc_in = d.accum; }
+          else { p = reinterpret_cast<float4*>(o2 + pix * c2 + (co - d.split)); acc_in = d.accum2; }
+          float4 w = v;
+          if (acc_in) {
+            const float4 a = *p;
+            w.x += a.x; w.y += a.y; w.z += a.z; w.w += a.w;
+          }
+          *p = w;
+        }
+      }
+    }
   } else if (d.out_mode == UNET_OUT_F32) {
     float* o1 = (float*)d.out;
     float* o2 = (float*)d.out2;
@@ -194,6 +231,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_des
   constexpr int E16 = 16 / (int)sizeof(T);
   static_assert(NT % NV == 0, "thread->channel-vector mapping must be fixed");
   __shared__ __attribute__((aligned(16))) T lds[2 * HP * RS];
+  static_assert(2 * HP * RS * sizeof(T) >= (size_t)(WM * WN) * 16 * (NTN * 16 + 4) * 4, "fp32 epilogue staging");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
