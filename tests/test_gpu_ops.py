@@ -83,12 +83,19 @@ def test_conv_fwd_act(prec, shape, k):
     ab = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2])
     w = (torch.randn(cout, cin, k, k, device="cuda") * 0.1).to(dt).float()
     out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
-    st = torch.empty(2, 4096, cout, device="cuda")
-    _conv(prec, [_act_src(y, ab)], N, H, W, cin, w, k, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
+    st = torch.zeros(2, 4096, cout, device="cuda")
+    d = _conv(prec, [_act_src(y, ab)], N, H, W, cin, w, k, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
     x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2)
     ref = F.conv2d(x, w, padding=k // 2).permute(0, 2, 3, 1)
     tol = 2e-2 if prec == "bf16" else 1e-4
     assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max()), (out.float() - ref).abs().max()
+    # BN partial sums ([2][Cout][rows], from the fp32 accumulators)
+    rows = L.load().unet_conv_stats_rows(d)
+    sums = st.flatten()[:2 * cout * rows].view(2, cout, rows).double().sum(-1)
+    r = ref.double().reshape(-1, cout)
+    P = r.shape[0]
+    assert ((sums[0] - r.sum(0)).abs() <= tol * P ** 0.5 * (1 + r.abs().mean(0))).all()
+    assert ((sums[1] - (r * r).sum(0)).abs() <= 4 * tol * (r * r).sum(0) + 1e-3).all()
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])
@@ -287,3 +294,102 @@ def test_conv_transpose_k2s2(prec, shape):
     assert (gb - m.bias.grad).abs().max() <= 1e-4 * (1 + m.bias.grad.abs().max())
     gx = x.grad.permute(0, 2, 3, 1)
     assert (a.grad - gx).abs().max() <= tol * (1 + gx.abs().max())
+
+
+# pointwise (1x1) path of csrc/pw.hip: taken for bf16 1x1 convs over >= 32768 pixels (the attention-gate
+# projections at 128^2..512^2); shapes include a pixel count that is not a multiple of the 256-pixel block
+PW_SHAPES = [(4, 128, 128, 64, 32), (4, 181, 183, 64, 64), (4, 128, 256, 128, 64), (8, 128, 128, 256, 128),
+             (4, 200, 170, 32, 64)]
+
+
+def _pw_var(L, d):
+    import ctypes
+    buf = ctypes.create_string_buffer(128)
+    L.load().unet_conv_variant(d, buf, 128)
+    return buf.value.decode()
+
+
+@pytest.mark.parametrize("shape", PW_SHAPES)
+@pytest.mark.parametrize("gate", [False, True])
+def test_pw_fwd_stats(shape, gate):
+    L = _lib()
+    N, H, W, cin, cout = shape
+    dt = torch.bfloat16
+    torch.manual_seed(5)
+    y = _rand(N, H, W, cin, dt=dt)
+    ab = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2])
+    src = _act_src(y, ab)
+    x = _act_ref(y, ab)
+    if gate:
+        p = torch.randn(N, H, W, device="cuda")
+        pab = torch.tensor([0.7, -0.1], device="cuda")
+        src.gate_p, src.gate_ab = p.data_ptr(), pab.data_ptr()
+        x = x * torch.sigmoid(p * 0.7 - 0.1)[..., None]
+    w = (torch.randn(cout, cin, 1, 1, device="cuda") * 0.1).to(dt).float()
+    out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
+    st = torch.zeros(2, cout, 8192, device="cuda")
+    d = _conv("bf16", [src], N, H, W, cin, w, 1, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
+    assert _pw_var(L, d).startswith("pw_conv_kernel"), _pw_var(L, d)
+    ref = F.conv2d(x.to(dt).float().permute(0, 3, 1, 2), w).permute(0, 2, 3, 1)
+    assert (out.float() - ref).abs().max() <= 2e-2 * (1 + ref.abs().max())
+    rows = L.load().unet_conv_stats_rows(d)
+    sums = st.flatten()[:2 * cout * rows].view(2, cout, rows).double().sum(-1)
+    r = ref.double().reshape(-1, cout)
+    assert torch.allclose(sums[0], r.sum(0), rtol=1e-3, atol=1e-1)
+    assert torch.allclose(sums[1], (r * r).sum(0), rtol=1e-3, atol=1e-1)
+
+
+@pytest.mark.parametrize("shape", PW_SHAPES)
+def test_pw_dgrad_split_accum(shape):
+    L = _lib()
+    N, H, W, cin, cout = shape     # forward 1x1 conv cin -> cout; dgrad dy[cout] -> dx[cin]
+    dt = torch.bfloat16
+    torch.manual_seed(6)
+    dy = _rand(N, H, W, cout, dt=dt)
+    w = (torch.randn(cout, cin, 1, 1, device="cuda") * 0.1).to(dt).float()
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w).permute(0, 2, 3, 1)
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    split = cin // 2
+    o1 = torch.full((N, H, W, split), 1.0, device="cuda")
+    o2 = torch.full((N, H, W, cin - split), float("nan"), device="cuda")
+    d = _conv("bf16", [src], N, H, W, cout, w, 1, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
+              split=split, accum=1, accum2=0)
+    if cout % 32 == 0:
+        assert _pw_var(L, d).startswith("pw_conv_kernel"), _pw_var(L, d)
+    got = torch.cat([o1 - 1.0, o2], -1)
+    assert (got - ref).abs().max() <= 2e-2 * (1 + ref.abs().max())
+
+
+@pytest.mark.parametrize("shape", PW_SHAPES)
+@pytest.mark.parametrize("gate", [False, True])
+def test_pw_wgrad(shape, gate):
+    L, R = _lib(), _rt()
+    N, H, W, cin, cout = shape
+    dt = torch.bfloat16
+    torch.manual_seed(7)
+    dy = _rand(N, H, W, cout, dt=dt)
+    ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
+    y = _rand(N, H, W, cin, dt=dt)
+    src = _act_src(y, ab)
+    x = _act_ref(y, ab)
+    if gate:
+        p = torch.randn(N, H, W, device="cuda")
+        pab = torch.tensor([0.7, -0.1], device="cuda")
+        src.gate_p, src.gate_ab = p.data_ptr(), pab.data_ptr()
+        x = x * torch.sigmoid(p * 0.7 - 0.1)[..., None]
+    x = x.to(dt).float().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(x, (cout, cin, 1, 1), dy.float().permute(0, 3, 1, 2))
+    wd = L.WgradDesc()
+    wd.dtype = R.BF16.code
+    wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = N, H, W, cin, cout, 1, 1
+    wd.src[0] = src
+    wd.dy = dy.data_ptr()
+    dw = torch.full((cout, cin, 1, 1), 3.0, device="cuda")
+    wd.dw = dw.data_ptr()
+    wd.accum = 1
+    ws = torch.empty(max(L.load().unet_wgrad_workspace(wd), 16), dtype=torch.uint8, device="cuda")
+    wd.workspace = ws.data_ptr()
+    L.call("unet_conv_wgrad", wd, R.stream())
+    torch.cuda.synchronize()
+    assert ((dw - 3.0) - ref).abs().max() <= 1e-3 * (1 + ref.abs().max()), float(((dw - 3.0) - ref).abs().max())

@@ -416,6 +416,10 @@ static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t s
 
 template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
 bool smallcin_conv_ok(const unet_conv_desc* d);  // smallcin.hip
+bool pw_conv_ok(const unet_conv_desc* d);        // pw.hip
+int pw_conv_rows(const unet_conv_desc* d);
+int pw_conv(const unet_conv_desc* d, hipStream_t st);
+int pw_conv_variant(const unet_conv_desc* d, char* buf, int len);
 int smallcin_rows(long long P);
 int smallcin_conv(const unet_conv_desc* d, hipStream_t st);
 
@@ -526,6 +530,7 @@ int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8)
 
 int unet_conv_stats_rows(const unet_conv_desc* d) {
   if (smallcin_conv_ok(d)) return smallcin_rows((long long)d->N * d->H * d->W);
+  if (pw_conv_ok(d)) return pw_conv_rows(d);
   if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
   const ConvCfg c = pick_cfg(d);
   return d->N * cdiv(d->W, CTW) * cdiv(d->H, 4 * c.wm);
@@ -536,6 +541,7 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
     snprintf(buf, len, "smallcin_fwd_kernel<%s>", d->dtype == UNET_BF16 ? "bf16" : "fp32");
     return 0;
   }
+  if (pw_conv_ok(d)) return pw_conv_variant(d, buf, len);
   if (!fast_eligible(d)) {
     snprintf(buf, len, "conv_generic_kernel<%s,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize,
              d->Cout <= 32 ? 32 : 64);
@@ -642,6 +648,7 @@ int unet_conv(const unet_conv_desc* d, void* stream) {
   }
   hipStream_t st = (hipStream_t)stream;
   if (smallcin_conv_ok(d)) return smallcin_conv(d, st);
+  if (pw_conv_ok(d)) return pw_conv(d, st);
   if (d->dtype == UNET_BF16) return dispatch_conv<bf16>(d, st);
   if (d->dtype == UNET_F32) return dispatch_conv<float>(d, st);
   set_error("unet_conv: bad dtype");

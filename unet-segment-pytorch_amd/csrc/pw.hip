@@ -1,0 +1,486 @@
+// pw.hip — pointwise (1x1) convolution fwd / dgrad / wgrad on MFMA for the attention-gate projections.
+//
+// Reference: AttentionGate W_g / W_x (nn.Conv2d(k=1, bias=False) + BN, unet/models/layers.py:151-160,
+// applied at :186-187) and their convolution_backward.  These are HBM-bound GEMMs (AI 21-169 FLOP/B
+// at bs 4, SURVEY §8(a) gate rows): the work is to stream the NHWC operands once at full width, so the
+// 1x1 case drops the 3x3 machinery (halo, LDS, per-chunk barriers) entirely:
+//  * fwd / dgrad: a 1x1 conv is a GEMM over the flattened pixel index, so a wave computes
+//    D[co][px] = W[co][ci] . X[ci][px] with the weight fragment as the MFMA A operand (the packed
+//    fragment-major layout, L2-resident) and the activation as the B operand, which is exactly one
+//    16-byte NHWC load per lane (8 channels of one pixel) — no LDS.  The virtual-activation transform
+//    (BN-apply + ReLU, x sigmoid(psi)) is applied in registers.  The accumulator lane then holds 4
+//    consecutive channels of one pixel: 8-byte bf16 stores (y) or 16-byte fp32 stores / read-modify-
+//    writes (dgrad), and the BN partial sums reduce over the 16 pixel lanes with shuffles;
+//  * wgrad: dW[co][ci] = sum_px dy[px][co] X[px][ci]: 64-pixel tiles of dy and X are staged in LDS
+//    (double-buffered, one barrier per tile) and read with the CDNA4 transposed read
+//    ds_read_b64_tr_b16 so the pixel index runs along K; split-K partial slabs are summed in a fixed
+//    order by wgrad_reduce2 (deterministic).
+#include "common.h"
+
+namespace unet {
+
+constexpr unsigned PW_OOB = 0x40000000u;  // >= every tensor byte size admitted below (< 1 GiB)
+typedef __amdgpu_buffer_rsrc_t pw_rsrc_t;
+
+__device__ __forceinline__ pw_rsrc_t pw_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 pw_ld(pw_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ unsigned pw_pack2(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  const bf16x2 p = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, p);
+}
+
+// 8 bf16 channels (one lane's 16-byte vector) through the source transform
+__device__ __forceinline__ bf16x8 pw_act(uint4 q, bool act, const float* sc, const float* sf, float lo, float gmul) {
+  if (!act && gmul == 1.f) return __builtin_bit_cast(bf16x8, q);
+  const unsigned u[4] = {q.x, q.y, q.z, q.w};
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(u[i] << 16);
+    v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+  }
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= gmul;
+  const uint4 r = make_uint4(pw_pack2(v[0], v[1]), pw_pack2(v[2], v[3]), pw_pack2(v[4], v[5]), pw_pack2(v[6], v[7]));
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// ------------------------------------------------------------------------------------------------
+// fwd / dgrad.  Block = 4 waves; wave = 16*NB pixels x 16*NA output channels; grid (P / (64*NB), Cout / (16*NA))
+// ------------------------------------------------------------------------------------------------
+template <int NA, int NB>
+__global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, long long P, int nchunks) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4;
+  const long long pw0 = ((long long)blockIdx.x * 4 + wave) * (16 * NB);
+  const int co0 = blockIdx.y * (16 * NA);
+  const unet_src& s = d.src[0];
+  const bool act = s.kind == UNET_SRC_ACT;
+  const float lo = s.relu ? 0.f : -INFINITY;
+  const unsigned pixb = (unsigned)d.Cin * 2u;
+  const pw_rsrc_t xr = pw_rsrc(s.data, (unsigned)(P * pixb));
+  // packed weights [ntile][chunk][64 lanes][16 B] (1x1: one tap)
+  const pw_rsrc_t wr = pw_rsrc(d.weight, (unsigned)((d.Cout + 127) / 128 * 8) * (unsigned)nchunks * 1024u);
+
+  // this lane's pixels (one per px tile) and their gate multipliers; pixels past P read as 0 (OOB) and
+  // are forced to 0 after the transform
+  unsigned xoff[NB];
+  float gm[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const long long p = pw0 + 16 * b + i16;
+    const bool ok = p < P;
+    xoff[b] = ok ? (unsigned)p * pixb + (unsigned)g * 16u : PW_OOB;
+    gm[b] = ok ? 1.f : 0.f;
+    if (ok && act && s.gate_p) gm[b] = sigmoidf_(s.gate_p[p] * s.gate_ab[0] + s.gate_ab[1]);
+  }
+
+  f32x4 acc[NA][NB];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 xq[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) xq[b] = pw_ld(xr, xoff[b], 0);
+  for (int c = 0; c < nchunks; ++c) {
+    uint4 xn[NB];
+    if (c + 1 < nchunks) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) xn[b] = pw_ld(xr, xoff[b], (unsigned)(c + 1) * 64u);
+    }
+    uint4 wq[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      wq[a] = pw_ld(wr, (unsigned)lane * 16u, ((unsigned)(co0 / 16 + a) * nchunks + c) * 1024u);
+    float sc[8], sf[8];
+    if (act) {
+      const int ch = c * 32 + g * 8;
+      const float4 s0 = *reinterpret_cast<const float4*>(s.scale + ch);
+      const float4 s1 = *reinterpret_cast<const float4*>(s.scale + ch + 4);
+      const float4 f0 = *reinterpret_cast<const float4*>(s.shift + ch);
+      const float4 f1 = *reinterpret_cast<const float4*>(s.shift + ch + 4);
+      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+      sf[0] = f0.x; sf[1] = f0.y; sf[2] = f0.z; sf[3] = f0.w; sf[4] = f1.x; sf[5] = f1.y; sf[6] = f1.z; sf[7] = f1.w;
+    }
+    bf16x8 xb[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) xb[b] = pw_act(xq[b], act, sc, sf, lo, gm[b]);
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      const bf16x8 wa = __builtin_bit_cast(bf16x8, wq[a]);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xb[b], acc[a][b], 0, 0, 0);
+    }
+    if (c + 1 < nchunks) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) xq[b] = xn[b];
+    }
+  }
+
+  // epilogue: acc[a][b][r] = out[px = pw0 + 16b + i16][co = co0 + 16a + 4g + r]
+  if (d.out_mode == UNET_OUT_Y) {
+    bf16* y = (bf16*)d.out;
+    float sm[NA][4], sq[NA][4];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { sm[a][r] = 0.f; sq[a][r] = 0.f; }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const long long p = pw0 + 16 * b + i16;
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const int co = co0 + 16 * a + 4 * g;
+        if (p < P) {
+          const f32x4 v = acc[a][b];
+          *reinterpret_cast<uint2*>(y + p * d.Cout + co) = make_uint2(pw_pack2(v[0], v[1]), pw_pack2(v[2], v[3]));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // pixels past P accumulated exact zeros
+          sm[a][r] += acc[a][b][r];
+          sq[a][r] += acc[a][b][r] * acc[a][b][r];
+        }
+      }
+    }
+    if (d.stats) {
+      __shared__ float red[4][NA * 16][2];
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float u = sm[a][r], w = sq[a][r];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) { u += __shfl_xor(u, o, 64); w += __shfl_xor(w, o, 64); }
+          if (i16 == 0) { red[wave][16 * a + 4 * g + r][0] = u; red[wave][16 * a + 4 * g + r][1] = w; }
+        }
+      __syncthreads();
+      if (tid < NA * 16) {
+        const int co = co0 + tid;
+        const float u = red[0][tid][0] + red[1][tid][0] + red[2][tid][0] + red[3][tid][0];
+        const float w = red[0][tid][1] + red[1][tid][1] + red[2][tid][1] + red[3][tid][1];
+        d.stats[(size_t)co * gridDim.x + blockIdx.x] = u;
+        d.stats[((size_t)d.Cout + co) * gridDim.x + blockIdx.x] = w;
+      }
+    }
+  } else {  // UNET_OUT_F32 (host-checked: split % 4 == 0)
+    float* o1 = (float*)d.out;
+    float* o2 = (float*)d.out2;
+    const int c2 = d.Cout - d.split;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const long long p = pw0 + 16 * b + i16;
+      if (p >= P) continue;
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const int co = co0 + 16 * a + 4 * g;
+        float4* q;
+        int acc_in;
+        if (co < d.split) { q = reinterpret_cast<float4*>(o1 + p * d.split + co); acc_in = d.accum; }
+        else { q = reinterpret_cast<float4*>(o2 + p * c2 + (co - d.split)); acc_in = d.accum2; }
+        float4 v = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+        if (acc_in) {
+          const float4 o = *q;
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        *q = v;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// wgrad.  Block = 4 waves owns dW[co0 .. co0+16*MA)[ci0 .. ci0+64*MB); wave w owns ci tiles
+// [w*MB, (w+1)*MB).  blockIdx.x = split (a contiguous range of 64-pixel tiles).
+// ------------------------------------------------------------------------------------------------
+constexpr int PW_KP = 64;  // pixels per staged tile
+
+__device__ __forceinline__ bf16x8 pw_tr8(const bf16* r0, const bf16* r1) {
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r0));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r1));
+  typedef __attribute__((ext_vector_type(8))) short i16x8;
+  const i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int MA, int MB>
+__global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, long long P, int per_split, float* ws) {
+  constexpr int BCO = 16 * MA, BCI = 64 * MB;
+  // LDS row strides: odd multiples of 32 B (see wgrad2.hip) so the tr reads are conflict-free
+  constexpr int RSD = BCO + (BCO % 32 == 0 ? 16 : 32 - BCO % 32 + 16);
+  constexpr int RSX = BCI + 16;
+  static_assert((RSD / 16) % 2 == 1 && (RSX / 16) % 2 == 1, "odd multiples of 32 B");
+  constexpr int NVD = BCO / 8, NVX = BCI / 8;              // 16-byte vectors per pixel row
+  constexpr int ID = (PW_KP * NVD + 255) / 256, IX = (PW_KP * NVX + 255) / 256;
+  constexpr int BUF = PW_KP * (RSD + RSX);
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int co0 = blockIdx.z * BCO, ci0 = blockIdx.y * BCI;
+  const long long ntiles = (P + PW_KP - 1) / PW_KP;
+  const long long t_begin = (long long)blockIdx.x * per_split;
+  const long long t_end = t_begin + per_split < ntiles ? t_begin + per_split : ntiles;
+  const unet_src& s = d.src[0];
+  const bool act = s.kind == UNET_SRC_ACT;
+  const float lo = s.relu ? 0.f : -INFINITY;
+  const unsigned xpix = (unsigned)d.Cin * 2u, dpix = (unsigned)d.Cout * 2u;
+  const pw_rsrc_t xr = pw_rsrc(s.data, (unsigned)(P * xpix));
+  const pw_rsrc_t dr = pw_rsrc(d.dy, (unsigned)(P * dpix));
+
+  // fixed per-thread channel vectors (NVX, NVD divide 256)
+  const int vx = tid % NVX, vd = tid % NVD;
+  const int cx = ci0 + vx * 8, cd = co0 + vd * 8;
+  const bool cx_ok = cx < d.Cin, cd_ok = cd < d.Cout;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = 1.f; sf[j] = 0.f; }
+  if (act && cx_ok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = s.scale[cx + j]; sf[j] = s.shift[cx + j]; }
+  }
+  uint4 qx[IX], qd[ID];
+  float gx[IX];
+  auto issue = [&](long long t) {
+    const long long pbase = t * PW_KP;
+#pragma unroll
+    for (int k = 0; k < IX; ++k) {
+      const int pr = (tid + 256 * k) / NVX;
+      const long long p = pbase + pr;
+      const bool ok = pr < PW_KP && p < P && cx_ok;
+      qx[k] = pw_ld(xr, ok ? (unsigned)p * xpix + (unsigned)cx * 2u : PW_OOB, 0);
+      gx[k] = ok ? 1.f : 0.f;
+      if (ok && act && s.gate_p) gx[k] = sigmoidf_(s.gate_p[p] * s.gate_ab[0] + s.gate_ab[1]);
+    }
+#pragma unroll
+    for (int k = 0; k < ID; ++k) {
+      const int pr = (tid + 256 * k) / NVD;
+      const long long p = pbase + pr;
+      const bool ok = pr < PW_KP && p < P && cd_ok;
+      qd[k] = pw_ld(dr, ok ? (unsigned)p * dpix + (unsigned)cd * 2u : PW_OOB, 0);
+    }
+  };
+  auto finish = [&](bf16* buf) {
+    bf16* bd = buf;
+    bf16* bx = buf + PW_KP * RSD;
+#pragma unroll
+    for (int k = 0; k < IX; ++k) {
+      const int pr = (tid + 256 * k) / NVX;
+      if (pr < PW_KP)
+        *reinterpret_cast<bf16x8*>(bx + pr * RSX + vx * 8) = pw_act(qx[k], act, sc, sf, lo, gx[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < ID; ++k) {
+      const int pr = (tid + 256 * k) / NVD;
+      if (pr < PW_KP) *reinterpret_cast<uint4*>(bd + pr * RSD + vd * 8) = qd[k];
+    }
+  };
+
+  f32x4 acc[MA][MB];
+#pragma unroll
+  for (int a = 0; a < MA; ++a)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (t_begin < t_end) {
+    issue(t_begin);
+    finish(lds);
+  }
+  __syncthreads();
+  // tr-read lane geometry: group g reads pixel rows k0 + 8g + q (+4); odd groups take the +4 half first
+  // (bank spread) — A and B apply the same K permutation, so the MFMA sums are unchanged
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+  const int sw = (g & 1) * 4;
+  for (long long t = t_begin; t < t_end; ++t) {
+    const int cur = (int)((t - t_begin) & 1);
+    const bf16* bd = lds + cur * BUF;
+    const bf16* bx = bd + PW_KP * RSD;
+    const bool has_next = t + 1 < t_end;
+    if (has_next) issue(t + 1);
+#pragma unroll
+    for (int k0 = 0; k0 < PW_KP; k0 += 32) {
+      const int r0 = k0 + 8 * g + q + sw, r1 = k0 + 8 * g + q + 4 - sw;
+      bf16x8 av[MA];
+#pragma unroll
+      for (int a = 0; a < MA; ++a) av[a] = pw_tr8(bd + r0 * RSD + 16 * a + p4, bd + r1 * RSD + 16 * a + p4);
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int col = 16 * (wave * MB + b) + p4;
+        const bf16x8 bv = pw_tr8(bx + r0 * RSX + col, bx + r1 * RSX + col);
+#pragma unroll
+        for (int a = 0; a < MA; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv, acc[a][b], 0, 0, 0);
+      }
+    }
+    if (has_next) finish(lds + (cur ^ 1) * BUF);
+    __syncthreads();
+  }
+
+  // slab ws[split][co][ci]; C layout: row (co) = 4*(l>>4)+r, col (ci) = l&15
+  float* slab = ws + (size_t)blockIdx.x * d.Cout * d.Cin;
+#pragma unroll
+  for (int a = 0; a < MA; ++a)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int ci = ci0 + 16 * (wave * MB + b) + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + 16 * a + 4 * (lane >> 4) + r;
+        if (co < d.Cout && ci < d.Cin) slab[(size_t)co * d.Cin + ci] = acc[a][b][r];
+      }
+    }
+}
+
+// out[g][e] (+)= sum over slabs s in [g*per, min(splits, (g+1)*per)) of ws[s][e], in slab order (deterministic).
+// One thread per (16-byte column, group): a split-K reduction of many slabs of a small weight gradient
+// runs as two such passes (splits -> PW_RG groups -> 1) instead of one long serial loop per column.
+constexpr int PW_RG = 32;
+__global__ void pw_slab_reduce_kernel(const float* ws, int splits, int per, long long total4, float* out, int accum) {
+  const long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  if (e >= total4) return;
+  const int s0 = g * per, s1 = min(splits, s0 + per);
+  const float4* w = reinterpret_cast<const float4*>(ws);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    const float4 v0 = w[(size_t)s * total4 + e], v1 = w[(size_t)(s + 1) * total4 + e];
+    const float4 v2 = w[(size_t)(s + 2) * total4 + e], v3 = w[(size_t)(s + 3) * total4 + e];
+    a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+    a.x += v1.x; a.y += v1.y; a.z += v1.z; a.w += v1.w;
+    a.x += v2.x; a.y += v2.y; a.z += v2.z; a.w += v2.w;
+    a.x += v3.x; a.y += v3.y; a.z += v3.z; a.w += v3.w;
+  }
+  for (; s < s1; ++s) {
+    const float4 v = w[(size_t)s * total4 + e];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  float4* o = reinterpret_cast<float4*>(out) + (size_t)g * total4 + e;
+  if (accum) {
+    const float4 b = *o;
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  *o = a;
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+static bool pw_src_ok(const unet_src& s, int C) {
+  return (s.kind == UNET_SRC_PLAIN || s.kind == UNET_SRC_ACT) && s.C == C && !(s.gate_p && s.kind != UNET_SRC_ACT);
+}
+
+// the large-pixel-count 1x1 cases (attention-gate projections at 128^2..512^2); smaller maps keep the
+// tiled conv2 / wgrad2 paths, which re-use weights across more pixels per workgroup
+bool pw_conv_ok(const unet_conv_desc* d) {
+  const long long P = (long long)d->N * d->H * d->W;
+  if (d->dtype != UNET_BF16 || d->ksize != 1 || d->nsrc != 1 || !pw_src_ok(d->src[0], d->Cin)) return false;
+  if (d->Cin % 32 || d->Cout % 16 || d->Cin > 256 || P < 32768) return false;
+  if (d->out_mode == UNET_OUT_F32) { if (d->split % 4) return false; }
+  else if (d->out_mode != UNET_OUT_Y) return false;
+  return (double)P * d->Cin * 2 < (double)PW_OOB;
+}
+
+static void pw_conv_geom(const unet_conv_desc* d, int& na, int& nb) {
+  na = d->Cout % 64 == 0 ? 4 : (d->Cout % 32 == 0 ? 2 : 1);
+  nb = 4;
+}
+
+int pw_conv_rows(const unet_conv_desc* d) {
+  int na, nb;
+  pw_conv_geom(d, na, nb);
+  return cdiv((long long)d->N * d->H * d->W, 64 * nb);
+}
+
+template <int NA, int NB>
+static int launch_pw(const unet_conv_desc* d, hipStream_t st) {
+  const long long P = (long long)d->N * d->H * d->W;
+  dim3 grid(cdiv(P, 64 * NB), d->Cout / (16 * NA));
+  hipLaunchKernelGGL((pw_conv_kernel<NA, NB>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+  return check_launch("pw_conv");
+}
+
+int pw_conv(const unet_conv_desc* d, hipStream_t st) {
+  int na, nb;
+  pw_conv_geom(d, na, nb);
+  if (na == 4) return launch_pw<4, 4>(d, st);
+  if (na == 2) return launch_pw<2, 4>(d, st);
+  return launch_pw<1, 4>(d, st);
+}
+
+int pw_conv_variant(const unet_conv_desc* d, char* buf, int len) {
+  int na, nb;
+  pw_conv_geom(d, na, nb);
+  snprintf(buf, len, "pw_conv_kernel<%d,%d>", na, nb);
+  return 0;
+}
+
+struct PwWPlan {
+  int ma, mb, splits, per_split;
+  size_t ws_bytes;
+};
+
+bool pw_wgrad_ok(const unet_wgrad_desc* d) {
+  const long long P = (long long)d->N * d->H * d->W;
+  if (d->dtype != UNET_BF16 || d->ksize != 1 || d->nsrc != 1 || !pw_src_ok(d->src[0], d->Cin)) return false;
+  if (d->Cin % 64 || d->Cout % 16 || P < 131072) return false;  // measured: wgrad2 wins at 128^2 x bs4
+  return (double)P * d->Cin * 2 < (double)PW_OOB && (double)P * d->Cout * 2 < (double)PW_OOB;
+}
+
+static PwWPlan pw_wplan(const unet_wgrad_desc* d) {
+  PwWPlan p{};
+  p.ma = d->Cout % 64 == 0 ? 4 : (d->Cout % 32 == 0 ? 2 : 1);
+  p.mb = d->Cin % 256 == 0 ? 4 : (d->Cin % 128 == 0 ? 2 : 1);
+  const long long P = (long long)d->N * d->H * d->W;
+  const long long ntiles = (P + PW_KP - 1) / PW_KP;
+  const long long blocks_out = (long long)(d->Cout / (16 * p.ma)) * (d->Cin / (64 * p.mb));
+  const size_t slab = (size_t)d->Cout * d->Cin * sizeof(float);
+  long long s = (1024 + blocks_out - 1) / blocks_out;            // ~1024 workgroups
+  const long long cap = (long long)(((size_t)64 << 20) / slab);  // slab traffic <= 64 MB
+  if (s > cap) s = cap;
+  if (s > ntiles) s = ntiles;
+  if (s < 1) s = 1;
+  p.per_split = cdiv(ntiles, s);
+  p.splits = cdiv(ntiles, p.per_split);
+  p.ws_bytes = slab * (p.splits + PW_RG);
+  return p;
+}
+
+size_t pw_wgrad_ws(const unet_wgrad_desc* d) { return pw_wplan(d).ws_bytes; }
+
+template <int MA, int MB>
+static int launch_pww(const unet_wgrad_desc* d, const PwWPlan& p, hipStream_t st) {
+  const long long P = (long long)d->N * d->H * d->W;
+  dim3 grid(p.splits, d->Cin / (64 * MB), d->Cout / (16 * MA));
+  hipLaunchKernelGGL((pw_wgrad_kernel<MA, MB>), grid, dim3(256), 0, st, *d, P, p.per_split, (float*)d->workspace);
+  return check_launch("pw_wgrad");
+}
+
+int pw_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
+  const PwWPlan p = pw_wplan(d);
+  int e;
+  if (p.ma == 4) e = p.mb == 4 ? launch_pww<4, 4>(d, p, st) : p.mb == 2 ? launch_pww<4, 2>(d, p, st) : launch_pww<4, 1>(d, p, st);
+  else if (p.ma == 2) e = p.mb == 4 ? launch_pww<2, 4>(d, p, st) : p.mb == 2 ? launch_pww<2, 2>(d, p, st) : launch_pww<2, 1>(d, p, st);
+  else e = p.mb == 4 ? launch_pww<1, 4>(d, p, st) : p.mb == 2 ? launch_pww<1, 2>(d, p, st) : launch_pww<1, 1>(d, p, st);
+  if (e) return e;
+  // slabs -> PW_RG partial slabs (written after the split slabs in the workspace) -> dw
+  const long long total = (long long)d->Cout * d->Cin, total4 = total / 4;
+  const float* ws = (const float*)d->workspace;
+  float* part = (float*)d->workspace + (size_t)p.splits * total;
+  const int per = cdiv(p.splits, PW_RG), groups = cdiv(p.splits, per);
+  hipLaunchKernelGGL(pw_slab_reduce_kernel, dim3(cdiv(total4, 256), groups), dim3(256), 0, st, ws, p.splits, per, total4,
+                     part, 0);
+  hipLaunchKernelGGL(pw_slab_reduce_kernel, dim3(cdiv(total4, 256), 1), dim3(256), 0, st, part, groups, groups, total4,
+                     d->dw, d->accum);
+  return check_launch("pw_slab_reduce");
+}
+
+}  // namespace unet

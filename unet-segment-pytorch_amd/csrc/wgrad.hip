@@ -226,6 +226,9 @@ static int launch_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
 bool wgrad2_eligible(const unet_wgrad_desc* d, size_t* ws_bytes);  // wgrad2.hip
 int wgrad2_run(const unet_wgrad_desc* d, hipStream_t st);
 bool smallcin_wgrad_ok(const unet_wgrad_desc* d);  // smallcin.hip
+bool pw_wgrad_ok(const unet_wgrad_desc* d);        // pw.hip
+size_t pw_wgrad_ws(const unet_wgrad_desc* d);
+int pw_wgrad(const unet_wgrad_desc* d, hipStream_t st);
 size_t smallcin_wgrad_ws(const unet_wgrad_desc* d);
 int smallcin_wgrad(const unet_wgrad_desc* d, hipStream_t st);
 
@@ -246,6 +249,7 @@ static int validate_src_w(const unet_src& s) {
 size_t unet_wgrad_workspace(const unet_wgrad_desc* d) {
   size_t b = 0;
   if (unet::smallcin_wgrad_ok(d)) return unet::smallcin_wgrad_ws(d);
+  if (unet::pw_wgrad_ok(d)) return unet::pw_wgrad_ws(d);
   if (unet::wgrad2_eligible(d, &b)) return b;
   return wg_plan(d).ws_bytes;
 }
@@ -264,6 +268,7 @@ int unet_conv_wgrad(const unet_wgrad_desc* d, void* stream) {
   if (csum != d->Cin) { set_error("unet_conv_wgrad: source channels != Cin"); return UNET_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
   if (unet::smallcin_wgrad_ok(d)) return unet::smallcin_wgrad(d, st);
+  if (unet::pw_wgrad_ok(d)) return unet::pw_wgrad(d, st);
   if (unet::wgrad2_eligible(d, nullptr)) return unet::wgrad2_run(d, st);
   if (d->dtype == UNET_BF16) return d->ksize == 3 ? launch_wgrad<bf16, 3>(d, st) : launch_wgrad<bf16, 1>(d, st);
   if (d->dtype == UNET_F32) return d->ksize == 3 ? launch_wgrad<float, 3>(d, st) : launch_wgrad<float, 1>(d, st);

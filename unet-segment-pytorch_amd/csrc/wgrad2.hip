@@ -249,6 +249,15 @@ __global__ void wgrad_reduce2_kernel(const float* ws, int splits, long long tota
   }
 }
 
+// dw (+)= the fixed-order sum of `splits` slabs of `total` floats
+int wgrad_reduce2_launch(const float* ws, int splits, long long total, float* dw, int accum, hipStream_t st) {
+  long long blocks = (total / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(wgrad_reduce2_kernel, dim3((int)blocks), dim3(256), 0, st, ws, splits, total, dw, accum);
+  return check_launch("wgrad_reduce2");
+}
+
 struct W2Plan {
   bool ok;
   int wco, wci, mi, raw, tiles_w, tiles_h, mtiles, splits, per_split;
@@ -321,13 +330,8 @@ int launch_wgrad2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
   if (d->ksize == 3) e = p.raw == 4 ? launch_w2_cfg<3, 4>(d, p, st) : launch_w2_cfg<3, 1>(d, p, st);
   else e = p.raw == 4 ? launch_w2_cfg<1, 4>(d, p, st) : launch_w2_cfg<1, 1>(d, p, st);
   if (e) return e;
-  const long long total = (long long)d->Cout * d->Cin * d->ksize * d->ksize;
-  long long blocks = (total / 4 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(wgrad_reduce2_kernel, dim3((int)blocks), dim3(256), 0, st, (const float*)d->workspace, p.splits,
-                     total, d->dw, d->accum);
-  return check_launch("wgrad_reduce2");
+  return wgrad_reduce2_launch((const float*)d->workspace, p.splits, (long long)d->Cout * d->Cin * d->ksize * d->ksize,
+                              d->dw, d->accum, st);
 }
 
 // entry points used by wgrad.hip (which keeps the generic kernel for fp32 / odd channel counts)
