@@ -393,3 +393,58 @@ def test_pw_wgrad(shape, gate):
     L.call("unet_conv_wgrad", wd, R.stream())
     torch.cuda.synchronize()
     assert ((dw - 3.0) - ref).abs().max() <= 1e-3 * (1 + ref.abs().max()), float(((dw - 3.0) - ref).abs().max())
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 64), (1, 37, 50, 16), (2, 32, 48, 128)])
+@pytest.mark.parametrize("accum", [0, 1])
+def test_outconv_bwd_vec(shape, accum):
+    """OutConv (1x1 + bias, layers.py:109-123) backward on a BN+ReLU source: dx, dW, db (bf16 operands)."""
+    L = _lib()
+    N, H, W, C = shape
+    K = 2
+    dt = torch.bfloat16
+    torch.manual_seed(8)
+    y = _rand(N, H, W, C, dt=dt)
+    ab = torch.stack([torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2])
+    w = torch.randn(K, C, device="cuda") * 0.1
+    dl = torch.randn(N, K, H, W, device="cuda")
+    a = _act_ref(y, ab)                                   # NHWC fp32
+    ref_dx = torch.einsum("nkhw,kc->nhwc", dl, w)
+    ref_dw = torch.einsum("nkhw,nhwc->kc", dl, a)
+    ref_db = dl.sum((0, 2, 3))
+    P = N * H * W
+    rows = L.load().unet_outconv_rows(P)
+    part = torch.zeros(rows, K + 1, max(C, K), device="cuda")
+    da = torch.full((N, H, W, C), 2.0, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    L.call("unet_outconv_bwd", L.BF16, N, H, W, C, K, y.data_ptr(), ab[0].data_ptr(), ab[1].data_ptr(), 1,
+           w.data_ptr(), dl.data_ptr(), da.data_ptr(), accum, part.data_ptr(), s)
+    dw, db = torch.empty(K, C, device="cuda"), torch.empty(K, device="cuda")
+    L.call("unet_outconv_bwd_finalize", part.data_ptr(), rows, C, K, dw.data_ptr(), db.data_ptr(), 0, s)
+    torch.cuda.synchronize()
+    assert ((da - 2.0 * accum) - ref_dx).abs().max() <= 1e-5 * (1 + ref_dx.abs().max())
+    assert (dw - ref_dw).abs().max() <= 1e-4 * (1 + ref_dw.abs().max())
+    assert (db - ref_db).abs().max() <= 1e-4 * (1 + ref_db.abs().max())
+
+
+@pytest.mark.parametrize("geo", [(2, 32, 32, 64, 64, 64), (1, 16, 20, 33, 41, 32), (2, 7, 9, 14, 18, 8),
+                                 (1, 25, 17, 50, 34, 12)])
+@pytest.mark.parametrize("accum", [0, 1])
+def test_upsample_bwd(geo, accum):
+    """Adjoint of bilinear x2 (align_corners=True) + F.pad into the skip's frame (layers.py:78,98-102)."""
+    L, R = _lib(), _rt()
+    N, h, w, Hp, Wp, C = geo
+    up_h, up_w = 2 * h, 2 * w
+    pt, pl = (Hp - up_h) // 2, (Wp - up_w) // 2
+    torch.manual_seed(9)
+    g = torch.randn(N, Hp, Wp, C, device="cuda")
+    x = torch.randn(N, C, h, w, device="cuda", requires_grad=True)
+    u = F.interpolate(x, size=(up_h, up_w), mode="bilinear", align_corners=True)
+    u = F.pad(u, [pl, Wp - up_w - pl, pt, Hp - up_h - pt])
+    u.backward(g.permute(0, 3, 1, 2))
+    ref = x.grad.permute(0, 2, 3, 1)
+    dx = torch.full((N, h, w, C), 1.5, device="cuda")
+    L.call("unet_upsample_bwd", N, C, h, w, up_h, up_w, pt, pl, Hp, Wp, R.up_scale(h, up_h), R.up_scale(w, up_w),
+           g.data_ptr(), dx.data_ptr(), accum, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert ((dx - 1.5 * accum) - ref).abs().max() <= 1e-5 * (1 + ref.abs().max())

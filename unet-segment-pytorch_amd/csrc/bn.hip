@@ -35,9 +35,21 @@ __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long lon
   __shared__ double sh[16];
   const int c = blockIdx.x;
   double s = 0, ss = 0;
-  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
-    s += stats[(size_t)c * rows + r];           // [2][C][rows]: contiguous over r
-    ss += stats[((size_t)C + c) * rows + r];
+  const float* s0 = stats + (size_t)c * rows;         // [2][C][rows]: contiguous over r
+  const float* s1 = stats + ((size_t)C + c) * rows;
+  const int B = blockDim.x;
+  int r = threadIdx.x;
+  // 4 rows per trip: the loads of a trip are independent (issued together), the fp64 adds stay in
+  // row order per thread (deterministic)
+  for (; r + 3 * B < rows; r += 4 * B) {
+    const float a0 = s0[r], a1 = s0[r + B], a2 = s0[r + 2 * B], a3 = s0[r + 3 * B];
+    const float b0 = s1[r], b1 = s1[r + B], b2 = s1[r + 2 * B], b3 = s1[r + 3 * B];
+    s += a0; s += a1; s += a2; s += a3;
+    ss += b0; ss += b1; ss += b2; ss += b3;
+  }
+  for (; r < rows; r += B) {
+    s += s0[r];
+    ss += s1[r];
   }
   s = block_sum_d(s, sh);
   ss = block_sum_d(ss, sh);
@@ -225,7 +237,17 @@ __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, 
   __shared__ double sh[16];
   const int c = blockIdx.x;
   double a = 0, b = 0;
-  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+  const int B = blockDim.x;
+  int r = threadIdx.x;
+  for (; r + 3 * B < rows; r += 4 * B) {  // 4 independent loads per trip, adds in row order
+    const float g0 = sum_g[(size_t)r * C + c], g1 = sum_g[(size_t)(r + B) * C + c];
+    const float g2 = sum_g[(size_t)(r + 2 * B) * C + c], g3 = sum_g[(size_t)(r + 3 * B) * C + c];
+    const float x0 = sum_gx[(size_t)r * C + c], x1 = sum_gx[(size_t)(r + B) * C + c];
+    const float x2 = sum_gx[(size_t)(r + 2 * B) * C + c], x3 = sum_gx[(size_t)(r + 3 * B) * C + c];
+    a += g0; a += g1; a += g2; a += g3;
+    b += x0; b += x1; b += x2; b += x3;
+  }
+  for (; r < rows; r += B) {
     a += sum_g[(size_t)r * C + c];
     b += sum_gx[(size_t)r * C + c];
   }

@@ -62,6 +62,55 @@ __global__ void upsample_bwd4_kernel(long long N, int C, int Hs, int Ws, int up_
   }
 }
 
+// same adjoint with the destination windows precomputed (host-checked: each window spans <= 8 rows /
+// columns, true for every x2-or-less upsample): the 8 row and 8 column weights (0 outside
+// the window, the padded frame or the source support) are computed once per element instead of inside
+// the 2-D loop, and only the nonzero taps issue loads
+__global__ __launch_bounds__(256) void upsample_bwd4w_kernel(long long N, int C, int Hs, int Ws, int up_h, int up_w,
+                                                             int pt, int pl, int Hp, int Wp, float sh, float sw,
+                                                             const float* dup, float* dx, int accum) {
+  const int C4 = C / 4;
+  const long long total = N * Hs * (long long)Ws * C4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int c4 = e % C4;
+    long long t = e / C4;
+    const int j = t % Ws;
+    t /= Ws;
+    const int i = t % Hs;
+    const long long n = t / Hs;
+    // u contributes to row i only if floor(sh*u) in {i-1, i}: u in [(i-1)/sh, (i+1)/sh] (+-1 guard)
+    const int ulo = max(0, (int)ceilf((float)(i - 1) / sh) - 1), uhi = min(up_h - 1, (int)floorf((float)(i + 1) / sh) + 1);
+    const int vlo = max(0, (int)ceilf((float)(j - 1) / sw) - 1), vhi = min(up_w - 1, (int)floorf((float)(j + 1) / sw) + 1);
+    float wy[8], wx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int u = ulo + k, v = vlo + k;
+      const int yy = u + pt, xx = v + pl;
+      wy[k] = (u <= uhi && yy >= 0 && yy < Hp) ? up_weight(sh, u, Hs, i) : 0.f;
+      wx[k] = (v <= vhi && xx >= 0 && xx < Wp) ? up_weight(sw, v, Ws, j) : 0.f;
+    }
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ky = 0; ky < 8; ++ky) {
+      if (wy[ky] == 0.f) continue;
+      const float4* row = reinterpret_cast<const float4*>(dup + ((n * Hp + ulo + ky + pt) * (long long)Wp) * C) + c4;
+#pragma unroll
+      for (int kx = 0; kx < 8; ++kx) {
+        if (wx[kx] == 0.f) continue;
+        const float4 g = row[(long long)(vlo + kx + pl) * C4];
+        const float w = wy[ky] * wx[kx];
+        acc.x += w * g.x; acc.y += w * g.y; acc.z += w * g.z; acc.w += w * g.w;
+      }
+    }
+    float4* o = reinterpret_cast<float4*>(dx) + e;
+    if (accum) {
+      const float4 a = *o;
+      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    *o = acc;
+  }
+}
+
 // NHWC gather adjoint: dx[n,i,j,c] (+)= Σ_{u,v} wy(u,i) wx(v,j) d_up[n, u+pt, v+pl, c]
 __global__ void upsample_bwd_kernel(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pt, int pl, int Hp,
                                     int Wp, float sh, float sw, const float* dup, float* dx, int accum) {
@@ -285,6 +334,79 @@ __global__ void outconv_bwd_kernel(long long P, int HW, int C, int CL, int K, co
         part[((size_t)blockIdx.y * (K + 1) + K) * C + k] = a;  // db stored in row K, column k
       }
       __syncthreads();
+    }
+  }
+}
+
+// vectorised form (bf16, C % 8 == 0, G = C/8 a power of two <= 256): a thread owns 8 channels of one
+// pixel per iteration — one 16-byte y load, two 16-byte da stores (or read-modify-writes); the K class
+// gradients of the pixel are loaded once per thread.  Same partial-sum table as outconv_bwd_kernel:
+// part[block][k][c] = Σ dl·a, part[block][K][k] = Σ dl (db).
+template <int KK>
+__global__ __launch_bounds__(256) void outconv_bwd_vec_kernel(long long P, int HW, int C, int G, const bf16* y,
+                                                              const float* sc, const float* sf, int relu,
+                                                              const float* w, const float* dl, float* da, int accum,
+                                                              float* part) {
+  constexpr int F = KK * 8 + KK;  // per-thread partials: dw[k][8], db[k]
+  __shared__ float sh[256 * F];
+  const int tid = threadIdx.x, v = tid % G, py = tid / G, R = 256 / G;
+  const int c0 = v * 8;
+  float s8[8], f8[8], wk[KK][8], dw[KK][8], db[KK];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s8[j] = sc ? sc[c0 + j] : 1.f;
+    f8[j] = sf ? sf[c0 + j] : 0.f;
+#pragma unroll
+    for (int k = 0; k < KK; ++k) { wk[k][j] = w[k * C + c0 + j]; dw[k][j] = 0.f; }
+  }
+#pragma unroll
+  for (int k = 0; k < KK; ++k) db[k] = 0.f;
+  const float lo = relu ? 0.f : -INFINITY;
+  const long long per = (P + gridDim.x - 1) / gridDim.x;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  for (long long q = p0 + py; q < p1; q += R) {
+    const long long n = q / HW, hw = q % HW;
+    float dlk[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) { dlk[k] = dl[(n * KK + k) * HW + hw]; db[k] += dlk[k]; }
+    float a[8];
+    load_vec<bf16>(y + q * C + c0, a);
+    float g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = fmaxf(a[j] * s8[j] + f8[j], lo);
+      g[j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KK; ++k) { g[j] += wk[k][j] * dlk[k]; dw[k][j] += dlk[k] * a[j]; }
+    }
+    float4* o = reinterpret_cast<float4*>(da + q * C + c0);
+    float4 g0 = make_float4(g[0], g[1], g[2], g[3]), g1 = make_float4(g[4], g[5], g[6], g[7]);
+    if (accum) {
+      const float4 a0 = o[0], a1 = o[1];
+      g0.x += a0.x; g0.y += a0.y; g0.z += a0.z; g0.w += a0.w;
+      g1.x += a1.x; g1.y += a1.y; g1.z += a1.z; g1.w += a1.w;
+    }
+    o[0] = g0;
+    o[1] = g1;
+  }
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sh[tid * F + k * 8 + j] = dw[k][j];
+    sh[tid * F + KK * 8 + k] = db[k];
+  }
+  __syncthreads();
+  // fixed-order sums over the R pixel rows: thread e < C*KK owns dw[k][c]; e < KK (extra) owns db[k]
+  for (int e = tid; e < C * KK + KK; e += 256) {
+    float acc = 0.f;
+    if (e < C * KK) {
+      const int k = e / C, c = e % C, vv = c / 8, j = c % 8;
+      for (int r = 0; r < R; ++r) acc += sh[(r * G + vv) * F + k * 8 + j];
+      part[((size_t)blockIdx.x * (KK + 1) + k) * C + c] = acc;
+    } else {
+      const int k = e - C * KK;
+      for (int r = 0; r < R; ++r) acc += sh[(r * G) * F + KK * 8 + k];  // channel-vector 0 of each row
+      part[((size_t)blockIdx.x * (KK + 1) + KK) * C + k] = acc;
     }
   }
 }
@@ -544,6 +666,13 @@ extern "C" {
 int unet_upsample_bwd(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pad_t, int pad_l, int Hp, int Wp,
                       float sh, float sw, const float* d_up, float* dx, int accum, void* stream) {
   const long long total = N * Hs * (long long)Ws * C;
+  // widest destination window of upsample_bwd4w: floor(2/scale) + 3 taps (scale 0: the whole map)
+  auto span = [](float sc, int up) { return sc > 0.f ? (int)floorf(2.f / sc) + 3 : up + 8; };
+  if (C % 4 == 0 && span(sh, up_h) <= 8 && span(sw, up_w) <= 8) {
+    hipLaunchKernelGGL(upsample_bwd4w_kernel, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream, N, C, Hs,
+                       Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
+    return check_launch("upsample_bwd");
+  }
   if (C % 4 == 0) {
     hipLaunchKernelGGL(upsample_bwd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream, N, C, Hs,
                        Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
@@ -602,6 +731,12 @@ int unet_outconv_bwd(int dtype, long long N, int H, int W, int C, int K, const v
   if (K > OC_MAXK || K < 1 || C < K) { set_error("unet_outconv_bwd: need 1 <= n_classes <= min(8, C)"); return UNET_ERR_UNSUPPORTED; }
   const long long P = N * H * (long long)W;
   const int cl = chan_lanes_m(C), rows = oc_rows(P);
+  const int G = (C % 8 == 0 && C / 8 <= 256 && ((C / 8) & (C / 8 - 1)) == 0) ? C / 8 : 0;
+  if (dtype == UNET_BF16 && G && K == 2) {
+    hipLaunchKernelGGL(outconv_bwd_vec_kernel<2>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, H * W, C, G,
+                       (const bf16*)y, scale, shift, relu, w, dl, da, accum, partial);
+    return check_launch("outconv_bwd");
+  }
   dim3 grid(cdiv(C, cl), rows);
   if (dtype == UNET_BF16)
     hipLaunchKernelGGL(outconv_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, H * W, C, cl, K,
