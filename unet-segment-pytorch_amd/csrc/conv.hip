@@ -26,14 +26,16 @@ constexpr int PACK_NPAD = 128;   // packed rows padded to the largest BN
 // epilogue shared by conv2 / conv3.  acc[i][j][r] (lane l): pixel (h0 + MI*wm + i, w0 + 4*(l>>4) + r),
 // channel co0 + (wn*NTN + j)*16 + (l&15).  Modes: y + BN partial sums, fp32 (split across the concat,
 // optionally accumulated), ConvTranspose2d shuffle, max-pool backward routing.
-template <typename T, int WM, int WN, int NTN, int MI = 4>
+// OM: the output mode when known at compile time (-1: dispatch on d.out_mode at run time)
+template <typename T, int WM, int WN, int NTN, int MI = 4, int OM = -1>
 __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&acc)[MI][NTN], T* lds, int tid,
                                               int lane, int wm, int wn, long long n, int h0, int w0, int co0,
                                               int mt, int mtiles) {
   constexpr int BN = WN * NTN * 16;
   // acc[i][j][r] (lane l): pixel (h0 + MI*wm + i, w0 + 4*(l>>4) + r), channel co0 + (wn*NTN + j)*16 + (l&15)
   const int ow_base = w0 + 4 * (lane >> 4);
-  if (d.out_mode == UNET_OUT_Y) {
+  auto is = [&](int m) { return OM < 0 ? d.out_mode == m : OM == m; };
+  if (is(UNET_OUT_Y)) {
     T* y = (T*)d.out;
     float s[NTN], ss[NTN];
 #pragma unroll
@@ -82,7 +84,7 @@ __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&a
         }
       }
     }
-  } else if (d.out_mode == UNET_OUT_F32 && (d.Cout % 4) == 0 && (d.split % 4) == 0) {
+  } else if (is(UNET_OUT_F32) && (d.Cout % 4) == 0 && (d.split % 4) == 0) {
     // fp32 gradients: each row of the wave's tile is transposed through a wave-private LDS slice so a
     // lane stores (or read-modify-writes) 4 consecutive channels of one pixel as one 16-byte access,
     // instead of 4-byte accesses strided by the pixel pitch
@@ -119,7 +121,7 @@ __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&a
         }
       }
     }
-  } else if (d.out_mode == UNET_OUT_F32) {
+  } else if (is(UNET_OUT_F32)) {
     float* o1 = (float*)d.out;
     float* o2 = (float*)d.out2;
     const int c2 = d.Cout - d.split;
@@ -146,7 +148,7 @@ __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&a
         }
       }
     }
-  } else if (d.out_mode == UNET_OUT_SHUFFLE2) {
+  } else if (is(UNET_OUT_SHUFFLE2)) {
 #pragma unroll MI
     for (int i = 0; i < MI; ++i) {
       const int oh = h0 + wm * MI + i;
@@ -160,6 +162,7 @@ __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&a
         }
       }
     }
+  } else if (!is(UNET_OUT_POOL_BWD)) {
   } else if (d.pool_code) {  // UNET_OUT_POOL_BWD with the argmax recorded by unet_materialize_pool
     const unet_src& ps = d.pool_src;
     float* da = (float*)d.out;
