@@ -227,6 +227,14 @@ int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, 
 int unet_materialize_pool(int dtype, const unet_src* src, long long N, int H, int W, void* out, uint8_t* code,
                           void* stream);
 
+/* ---- segmentation metrics — SegmentationMetrics.update, metrics.py:55-84 ----------------------- */
+/* confusion[t][p] += #pixels with target t, predicted class p (argmax over the K fp32 NCHW logits,
+ * or the int64 labels when logits == NULL); pixels with t == ignore_index (has_ignore != 0) or a class
+ * outside [0, K) are skipped.  confusion: int64 [K][K] on the device, accumulated (never cleared).  */
+int unet_confusion_matrix(long long N, int K, long long HW, const float* logits, const int64_t* labels,
+                          const int64_t* targets, long long ignore_index, int has_ignore, int64_t* confusion,
+                          void* stream);
+
 /* ---- DiceBCE / Dice / BalancedCE loss + grad — loss.py:18-191 ------------------------------- */
 int unet_loss_rows(long long HW);
 /* pass 1: per-image partial sums (fp32 NCHW logits, int64 targets)                               */

@@ -1,0 +1,69 @@
+"""On-device confusion matrix / segmentation metrics (csrc/metrics.hip, unet/utils/metrics.py) against
+the reference's definitions (unet/utils/metrics.py:55-231) as restated in oracle/unet_oracle.py and
+the committed fixture tests/golden/metrics.pt.  Integer counts: bit-exact."""
+
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def _o():
+    from oracle import unet_oracle as O
+    return O
+
+
+def test_confusion_golden_fixture():
+    from unet.utils.metrics import SegmentationMetrics
+    g = torch.load(GOLD / "metrics.pt", weights_only=True)
+    m = SegmentationMetrics(num_classes=2)
+    m.update(g["z"].cuda(), g["t"].cuda())
+    assert np.array_equal(m.get_confusion_matrix(), g["confusion"].numpy())
+    r = m.compute()
+    assert r["mean_dice"] == pytest.approx(float(g["mean_dice"]), abs=1e-12)
+    assert r["mean_iou"] == pytest.approx(float(g["mean_iou"]), abs=1e-12)
+
+
+@pytest.mark.parametrize("shape", [(4, 2, 512, 512), (3, 2, 37, 53), (2, 5, 64, 80)])
+def test_confusion_matches_oracle(shape):
+    from unet.utils.metrics import SegmentationMetrics, compute_dice, compute_iou
+    O = _o()
+    N, K, H, W = shape
+    gen = torch.Generator().manual_seed(11)
+    z = torch.randn(N, K, H, W, generator=gen)
+    z[0, :, :3, :3] = 0.25                         # ties: the first maximum wins
+    t = torch.randint(0, K, (N, H, W), generator=gen)
+    m = SegmentationMetrics(num_classes=K)
+    m.update(z.cuda(), t.cuda())
+    m.update(z.argmax(1).cuda(), t.cuda())         # class-index input, accumulated
+    ref = O.confusion_matrix(z.argmax(1), t, K) * 2
+    assert np.array_equal(m.get_confusion_matrix(), ref.numpy())
+    # per-class IoU / Dice of metrics.py:160-231 (float32 counts, smoothing 1e-6)
+    p = z.argmax(1)
+    ious = torch.stack([((p == c) & (t == c)).float().sum().add(1e-6) / ((p == c) | (t == c)).float().sum().add(1e-6)
+                        for c in range(K)])
+    dices = torch.stack([(2.0 * ((p == c).float() * (t == c).float()).sum() + 1e-6) /
+                         ((p == c).float().sum() + (t == c).float().sum() + 1e-6) for c in range(K)])
+    assert torch.equal(compute_iou(z.cuda(), t.cuda(), K).cpu(), ious)
+    assert torch.equal(compute_dice(z.cuda(), t.cuda(), K).cpu(), dices)
+
+
+def test_confusion_ignore_index_and_out_of_range():
+    from unet.utils.metrics import SegmentationMetrics
+    O = _o()
+    gen = torch.Generator().manual_seed(12)
+    z = torch.randn(2, 2, 40, 40, generator=gen)
+    t = torch.randint(0, 2, (2, 40, 40), generator=gen)
+    t[0, :5] = 255                                  # ignored
+    t[1, :2] = 7                                    # out of range: skipped like the reference loop
+    m = SegmentationMetrics(num_classes=2, ignore_index=255)
+    m.update(z.cuda(), t.cuda())
+    keep = (t != 255) & (t < 2)
+    ref = O.confusion_matrix(z.argmax(1)[keep], t[keep], 2)
+    assert np.array_equal(m.get_confusion_matrix(), ref.numpy())
+    m.reset()
+    assert m.compute()["mean_dice"] == 0.0

@@ -1,6 +1,9 @@
-"""Hot-path utilities (reference: unet/utils/__init__.py).  Only the losses are part of this build;
-the reference's host-side metrics/callbacks/plots are out of scope."""
+"""Hot-path utilities (reference: unet/utils/__init__.py): the losses and the segmentation metrics
+(confusion matrix counted on the device).  The reference's host-side callbacks/plots/dataset are out
+of scope."""
 
 from .loss import DiceLoss, BalancedCELoss, DiceBCELoss, DeepSupervisionLoss, create_loss_function
+from .metrics import SegmentationMetrics, compute_dice, compute_iou
 
-__all__ = ["DiceLoss", "BalancedCELoss", "DiceBCELoss", "DeepSupervisionLoss", "create_loss_function"]
+__all__ = ["DiceLoss", "BalancedCELoss", "DiceBCELoss", "DeepSupervisionLoss", "create_loss_function",
+           "SegmentationMetrics", "compute_iou", "compute_dice"]

@@ -1,0 +1,149 @@
+"""Segmentation metrics on the device (reference: unet/utils/metrics.py).
+
+`SegmentationMetrics` keeps the reference's API (metrics.py:16-158): `update(predictions, targets)`
+accumulates a K x K int64 confusion matrix, `compute()` returns pixel accuracy, per-class and mean
+IoU / Dice with the same formulas (metrics.py:86-143, classes whose score is exactly 0 are left out of
+the means, :131-135).  The difference is where the counting runs: the reference moves every batch to the
+host and walks the pixels in a Python loop (metrics.py:78-84); here `update` is one HIP launch
+(`unet_confusion_matrix`: argmax over the logits + LDS histogram + 64-bit atomics) that accumulates into
+a device tensor without synchronising, and only `compute()` / `get_confusion_matrix()` read it back.
+Counts are integers, so the matrix is bit-identical to the reference's.
+
+`compute_iou` / `compute_dice` (metrics.py:160-231) are built on the same kernel.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .._hip import lib as L
+from .._hip.runtime import require_device, stream
+
+__all__ = ["SegmentationMetrics", "compute_iou", "compute_dice", "confusion_matrix"]
+
+
+def confusion_matrix(predictions: torch.Tensor, targets: torch.Tensor, num_classes: int = 2,
+                     ignore_index: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """int64 [K, K] device tensor, confusion[t, p] (+)= pixel counts (into `out` when given).
+
+    predictions: logits (N, C, H, W) — argmax over dim 1 — or class indices (N, H, W)."""
+    require_device(predictions, "predictions")
+    require_device(targets, "targets")
+    K = int(num_classes)
+    if out is None:
+        out = torch.zeros(K, K, dtype=torch.int64, device=predictions.device)
+    t = targets.to(torch.int64).contiguous()
+    if predictions.dim() == 4:
+        z = predictions.detach().float().contiguous()
+        N, C, H, W = z.shape
+        if C != K:
+            raise ValueError(f"logits have {C} channels, metrics were set up for {K} classes")
+        logits, labels = z.data_ptr(), None
+    else:
+        p = predictions.detach().to(torch.int64).contiguous()
+        N = p.shape[0]
+        H, W = 1, p.numel() // max(N, 1)
+        logits, labels = None, p.data_ptr()
+    if t.numel() != N * H * W:
+        raise ValueError(f"targets have {t.numel()} elements, predictions describe {N * H * W} pixels")
+    L.call("unet_confusion_matrix", N, K, H * W, logits, labels, t.data_ptr(),
+           int(ignore_index) if ignore_index is not None else 0, int(ignore_index is not None), out.data_ptr(),
+           stream())
+    return out
+
+
+class SegmentationMetrics:
+    """Accumulates a confusion matrix over batches and computes segmentation metrics
+    (reference: metrics.py:16-158; same constructor, methods and result keys)."""
+
+    def __init__(self, num_classes: int = 2, class_names: Optional[List[str]] = None,
+                 ignore_index: Optional[int] = None):
+        self.num_classes = num_classes
+        self.class_names = class_names or [f'class_{i}' for i in range(num_classes)]
+        self.ignore_index = ignore_index
+        self._cm: Optional[torch.Tensor] = None   # device int64 accumulator
+
+    @property
+    def confusion_matrix(self) -> np.ndarray:
+        """confusion[i, j] = pixels with true class i predicted as class j (host copy)."""
+        if self._cm is None:
+            return np.zeros((self.num_classes, self.num_classes), dtype=np.int64)
+        return self._cm.cpu().numpy()
+
+    def reset(self) -> None:
+        """Reset accumulated statistics."""
+        self._cm = None
+
+    def update(self, predictions: torch.Tensor, targets: torch.Tensor) -> None:
+        """Add a batch: logits (N, C, H, W) or class indices (N, H, W); targets (N, H, W)."""
+        if self._cm is None or self._cm.device != predictions.device:
+            self._cm = torch.zeros(self.num_classes, self.num_classes, dtype=torch.int64, device=predictions.device)
+        confusion_matrix(predictions, targets, self.num_classes, self.ignore_index, out=self._cm)
+
+    def compute(self) -> Dict[str, float]:
+        """pixel_accuracy, mean_iou, mean_dice, class_iou, class_dice (metrics.py:86-143)."""
+        cm = self.confusion_matrix
+        total = cm.sum()
+        if total == 0:
+            return self._empty_results()
+        pixel_accuracy = np.diag(cm).sum() / total
+        class_iou, class_dice = {}, {}
+        for i in range(self.num_classes):
+            tp = cm[i, i]
+            fp = cm[:, i].sum() - tp
+            fn = cm[i, :].sum() - tp
+            iou_denom = tp + fp + fn
+            iou = tp / iou_denom if iou_denom > 0 else 0.0
+            dice_denom = 2 * tp + fp + fn
+            dice = 2 * tp / dice_denom if dice_denom > 0 else 0.0
+            class_iou[self.class_names[i]] = iou
+            class_dice[self.class_names[i]] = dice
+        valid_ious = [v for v in class_iou.values() if v > 0]
+        valid_dices = [v for v in class_dice.values() if v > 0]
+        mean_iou = np.mean(valid_ious) if valid_ious else 0.0
+        mean_dice = np.mean(valid_dices) if valid_dices else 0.0
+        return {
+            'pixel_accuracy': float(pixel_accuracy),
+            'mean_iou': float(mean_iou),
+            'mean_dice': float(mean_dice),
+            'class_iou': class_iou,
+            'class_dice': class_dice,
+        }
+
+    def _empty_results(self) -> Dict[str, float]:
+        return {
+            'pixel_accuracy': 0.0,
+            'mean_iou': 0.0,
+            'mean_dice': 0.0,
+            'class_iou': {name: 0.0 for name in self.class_names},
+            'class_dice': {name: 0.0 for name in self.class_names},
+        }
+
+    def get_confusion_matrix(self) -> np.ndarray:
+        """Return the confusion matrix (host copy)."""
+        return self.confusion_matrix.copy()
+
+
+def _class_counts(predictions: torch.Tensor, targets: torch.Tensor, num_classes: int):
+    cm = confusion_matrix(predictions, targets, num_classes).to(torch.float32)
+    tp = torch.diagonal(cm)
+    pred = cm.sum(0)     # pixels predicted as class c
+    true = cm.sum(1)     # pixels labelled class c
+    return tp, pred, true
+
+
+def compute_iou(predictions: torch.Tensor, targets: torch.Tensor, num_classes: int = 2,
+                smooth: float = 1e-6) -> torch.Tensor:
+    """Per-class (I + s) / (U + s), U = |pred ∪ target| (metrics.py:160-193)."""
+    tp, pred, true = _class_counts(predictions, targets, num_classes)
+    return (tp + smooth) / ((pred + true - tp) + smooth)
+
+
+def compute_dice(predictions: torch.Tensor, targets: torch.Tensor, num_classes: int = 2,
+                 smooth: float = 1e-6) -> torch.Tensor:
+    """Per-class (2I + s) / (|pred| + |target| + s) (metrics.py:196-231)."""
+    tp, pred, true = _class_counts(predictions, targets, num_classes)
+    return (2.0 * tp + smooth) / ((pred + true) + smooth)
