@@ -17,6 +17,7 @@ Rank 0 prints one JSON line (value = whole-job images/s, max-over-ranks time).  
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -94,6 +95,8 @@ def main():
     ap.add_argument("--model", default="attention_unet", choices=["attention_unet", "unet"])
     ap.add_argument("--batch", type=int, default=4, help="per-GPU batch")
     ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--in-ch", type=int, default=1, help="input channels (C5: 3)")
+    ap.add_argument("--accum", type=int, default=1, help="micro-batches per optimizer step (C5: 8; scripts/train.py:133-143)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--probe", default=None, help="kernel family to time live (default: conv_kernel<prec,3,64>)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -114,7 +117,7 @@ def main():
     from unet.utils.loss import DiceBCELoss
 
     torch.manual_seed(0)
-    model = (AttentionUNet(1, 2) if args.model == "attention_unet" else UNet(1, 2)).to(dev).train()
+    model = (AttentionUNet(args.in_ch, 2) if args.model == "attention_unet" else UNet(args.in_ch, 2)).to(dev).train()
     model.hip_precision = args.precision
     net = model
     if world > 1:
@@ -123,13 +126,19 @@ def main():
     opt = torch.optim.AdamW(model.parameters(), lr=5e-5, weight_decay=1e-4, fused=True)
     crit = DiceBCELoss()
     gen = torch.Generator().manual_seed(1234 + rank)
-    x = (torch.rand(args.batch, 1, args.size, args.size, generator=gen) * 2 - 1).to(dev)
+    x = (torch.rand(args.batch, args.in_ch, args.size, args.size, generator=gen) * 2 - 1).to(dev)
     t = disc_targets(args.batch, args.size, args.size, gen).to(dev)
     params = list(model.parameters())
 
     def step():
-        loss = crit(net(x), t)
-        loss.backward()
+        # grad accumulation as scripts/train.py:133-143: loss / accum per micro-batch, gradients
+        # all-reduced once per optimizer step (DDP no_sync on the first accum-1 micro-batches)
+        for k in range(args.accum):
+            last = k == args.accum - 1
+            ctx = net.no_sync() if (world > 1 and not last) else contextlib.nullcontext()
+            with ctx:
+                loss = crit(net(x), t)
+                (loss / args.accum if args.accum > 1 else loss).backward()
         torch.nn.utils.clip_grad_norm_(params, 1.0)
         opt.step()
         opt.zero_grad(set_to_none=True)
@@ -153,7 +162,7 @@ def main():
     elapsed = max_over_ranks(elapsed, dev)
     ps = probe.summary()
 
-    images = world * args.batch * args.steps
+    images = world * args.batch * args.accum * args.steps
     value = images / elapsed
     peak = MFMA_PEAK_TFLOPS[args.precision]
     achieved = ps["tflops"] or 0.0
@@ -161,18 +170,23 @@ def main():
     tfile = ROOT / "profiles" / "traffic.json"
     if tfile.exists():
         tr = json.loads(tfile.read_text())
-        traffic = tr.get(target)
+        ent = tr.get(target)
+        traffic = ent.get("bytes_per_launch") if isinstance(ent, dict) else ent
     line = {
         "metric": "512x512 CT slices/sec fwd+bwd, AttentionUNet bs=4/GPU, 1/2/4/8 MI355X",
         "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic (x~U(-1,1), 1-3 disc masks/img; seeded)",
-        "config": {"workload": f"{args.model} 1x{args.size}x{args.size} train step (fwd+DiceBCE+bwd+clip+AdamW)",
-                   "model": args.model, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                   "image": [1, args.size, args.size], "parallelism": f"dp{world}" if world > 1 else "single"},
-        "whole_step_tflops": round(value * FLOPS_PER_IMAGE[args.model] / 1e12, 2),
+        "config": {"workload": f"{args.model} {args.in_ch}x{args.size}x{args.size} train step "
+                               f"(fwd+DiceBCE+bwd{' x%d accum' % args.accum if args.accum > 1 else ''}+clip+AdamW)",
+                   "model": args.model, "global_batch": world * args.batch * args.accum, "per_gpu_batch": args.batch,
+                   "grad_accum": args.accum, "image": [args.in_ch, args.size, args.size],
+                   "parallelism": f"dp{world}" if world > 1 else "single"},
+        "whole_step_tflops": (round(value * FLOPS_PER_IMAGE[args.model] / 1e12, 2)
+                              if (args.size, args.in_ch) == (512, 1) else None),
         "roofline": {"kernel": target, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, profiles/traffic.json)",
                      "launches": ps["launches"], "avg_us": round(ps["avg_us"], 2) if ps["avg_us"] else None,
                      "flops_per_launch": round(ps["flops"] / ps["launches"]) if ps["launches"] else None},
         "final_loss": round(float(loss.detach()), 5),
