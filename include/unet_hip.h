@@ -143,9 +143,10 @@ int unet_bn_eval_affine(int C, const float* gamma, const float* beta, const floa
                         const float* running_var, float eps, float* scale, float* shift, void* stream);
 /* backward: g = da * [scale*y+shift > 0] (relu!=0) ; partial sums of g and g*xhat              */
 int unet_bn_bwd_reduce_rows(long long P, int C);
-int unet_bn_bwd_reduce(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
-                       const float* shift, int relu, const float* mean, const float* invstd,
-                       float* partial, void* stream);
+/* da: gradient w.r.t. the activation, fp32 (da_dtype UNET_F32) or bf16 (UNET_BF16, with dtype UNET_BF16) */
+int unet_bn_bwd_reduce(int dtype, int da_dtype, long long P, int C, const void* da, const void* y,
+                       const float* scale, const float* shift, int relu, const float* mean,
+                       const float* invstd, float* partial, void* stream);
 /* -> dgamma, dbeta (fp32 [C], stored or accumulated) and coef[3][C] with dy = A*g + B*y + Cc    */
 int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
                          const float* gamma, const float* mean, const float* invstd, float* dgamma,
@@ -153,8 +154,8 @@ int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int 
 /* column sums of a [rows][C] fp32 partial table (fp64 accumulation): out (+)= sum_r part[r][:]    */
 int unet_colsum(const float* part, int rows, int C, float* out, int accum, void* stream);
 /* dy (op dtype) = A*g + B*y + Cc                                                                */
-int unet_bn_bwd_apply(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
-                      const float* shift, int relu, const float* coef, void* dy, void* stream);
+int unet_bn_bwd_apply(int dtype, int da_dtype, long long P, int C, const void* da, const void* y,
+                      const float* scale, const float* shift, int relu, const float* coef, void* dy, void* stream);
 
 /* ---- attention gate (AttentionGate.forward/backward) — layers.py:171-192 ---------------------- */
 /* p = sum_c wpsi_c * relu(sg*gw+bg + sx*xw+bx) ; partial sums of p                               */

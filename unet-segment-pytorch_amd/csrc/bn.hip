@@ -100,8 +100,8 @@ static inline int reduce_rows(long long P, int C) {
   return (int)r;
 }
 
-template <typename T>
-__global__ void bn_bwd_reduce_kernel(long long P, int C, int CL, const float* da, const T* y, const float* scale,
+template <typename T, typename G>
+__global__ void bn_bwd_reduce_kernel(long long P, int C, int CL, const G* da, const T* y, const float* scale,
                                      const float* shift, int relu, const float* mean, const float* invstd, float* part,
                                      int rows) {
   __shared__ float sh[2][256];
@@ -115,7 +115,7 @@ __global__ void bn_bwd_reduce_kernel(long long P, int C, int CL, const float* da
     const float sc = scale[c], sf = shift[c], mu = mean[c], is = invstd[c];
     for (long long p = p0 + py; p < p1; p += R) {
       const float yv = to_f(y[p * C + c]);
-      float g = da[p * C + c];
+      float g = to_f(da[p * C + c]);
       if (relu && !(yv * sc + sf > 0.f)) g = 0.f;
       sg += g;
       sgx += g * (yv - mu) * is;
@@ -132,10 +132,16 @@ __global__ void bn_bwd_reduce_kernel(long long P, int C, int CL, const float* da
   }
 }
 
+// 8 gradient values (fp32: two 16-byte loads; bf16: one)
+template <typename G> __device__ __forceinline__ void load8(const G* p, float* v) {
+  load_vec<G>(p, v);
+  if constexpr (sizeof(G) == 4) load_vec<G>(p + 4, v + 4);
+}
+
 // vectorised forms (C % 8 == 0): a thread owns 8 channels (16-byte y, 2 x 16-byte da) of one pixel;
 // the block covers 256 / (C/8) pixels per iteration with a fixed channel vector per thread
-template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int C, const float* da, const T* y,
+template <typename T, typename G>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int C, const G* da, const T* y,
                                                                 const float* scale, const float* shift, int relu,
                                                                 const float* mean, const float* invstd, float* part,
                                                                 int rows) {
@@ -156,8 +162,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int
       float yv[8], g[8];
       load_vec<T>(y + p * C + cv * 8, yv);
       if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
-      load_vec<float>(da + p * C + cv * 8, g);
-      load_vec<float>(da + p * C + cv * 8 + 4, g + 4);
+      load8<G>(da + p * C + cv * 8, g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[j];
@@ -182,8 +187,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int C, const float* da, const T* y,
+template <typename T, typename G>
+__global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int C, const G* da, const T* y,
                                                                const float* scale, const float* shift, int relu,
                                                                const float* coef, T* dy) {
   const int CV = C / 8;
@@ -202,8 +207,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int 
     float yv[8], g[8], o[8];
     load_vec<T>(y + p * C + cv * 8, yv);
     if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
-    load_vec<float>(da + p * C + cv * 8, g);
-    load_vec<float>(da + p * C + cv * 8 + 4, g + 4);
+    load8<G>(da + p * C + cv * 8, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[j];
@@ -267,8 +271,8 @@ __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, 
   }
 }
 
-template <typename T>
-__global__ void bn_bwd_apply_kernel(long long P, int C, int CL, const float* da, const T* y, const float* scale,
+template <typename T, typename G>
+__global__ void bn_bwd_apply_kernel(long long P, int C, int CL, const G* da, const T* y, const float* scale,
                                     const float* shift, int relu, const float* coef, T* dy, int rows) {
   const int tid = threadIdx.x;
   const int cx = tid % CL, py = tid / CL, R = blockDim.x / CL;
@@ -279,7 +283,7 @@ __global__ void bn_bwd_apply_kernel(long long P, int C, int CL, const float* da,
   const float sc = scale[c], sf = shift[c], A = coef[c], B = coef[C + c], Cc = coef[2 * C + c];
   for (long long p = p0 + py; p < p1; p += R) {
     const float yv = to_f(y[p * C + c]);
-    float g = da[p * C + c];
+    float g = to_f(da[p * C + c]);
     if (relu && !(yv * sc + sf > 0.f)) g = 0.f;
     dy[p * C + c] = from_f<T>(A * g + B * yv + Cc);
   }
@@ -322,26 +326,34 @@ int unet_bn_eval_affine(int C, const float* gamma, const float* beta, const floa
 
 int unet_bn_bwd_reduce_rows(long long P, int C) { return bn_vec_ok(C) ? reduce_rows_vec(P, C) : reduce_rows(P, C); }
 
-int unet_bn_bwd_reduce(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
+int unet_bn_bwd_reduce(int dtype, int da_dtype, long long P, int C, const void* da, const void* y, const float* scale,
                        const float* shift, int relu, const float* mean, const float* invstd, float* partial,
                        void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == UNET_F32 && da_dtype != UNET_F32) { set_error("unet_bn_bwd_reduce: bf16 gradient needs bf16 y"); return UNET_ERR_ARG; }
   if (bn_vec_ok(C)) {
     const int rows = reduce_rows_vec(P, C);
-    if (dtype == UNET_BF16)
-      hipLaunchKernelGGL(bn_bwd_reduce_vec_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, C, da,
+    if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
+      hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<bf16, bf16>), dim3(rows), dim3(256), 0, st, P, C, (const bf16*)da,
+                         (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
+    else if (dtype == UNET_BF16)
+      hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<bf16, float>), dim3(rows), dim3(256), 0, st, P, C, (const float*)da,
                          (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
     else
-      hipLaunchKernelGGL(bn_bwd_reduce_vec_kernel<float>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, C, da,
+      hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<float, float>), dim3(rows), dim3(256), 0, st, P, C, (const float*)da,
                          (const float*)y, scale, shift, relu, mean, invstd, partial, rows);
     return check_launch("bn_bwd_reduce");
   }
   const int cl = chan_lanes(C), rows = reduce_rows(P, C);
   dim3 grid(cdiv(C, cl), rows);
-  if (dtype == UNET_BF16)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, C, cl, da,
+  if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, bf16>), grid, dim3(256), 0, st, P, C, cl, (const bf16*)da,
+                       (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
+  else if (dtype == UNET_BF16)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
                        (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, P, C, cl, da,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
                        (const float*)y, scale, shift, relu, mean, invstd, partial, rows);
   return check_launch("bn_bwd_reduce");
 }
@@ -354,26 +366,34 @@ int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int 
   return check_launch("bn_bwd_finalize");
 }
 
-int unet_bn_bwd_apply(int dtype, long long P, int C, const float* da, const void* y, const float* scale,
+int unet_bn_bwd_apply(int dtype, int da_dtype, long long P, int C, const void* da, const void* y, const float* scale,
                       const float* shift, int relu, const float* coef, void* dy, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == UNET_F32 && da_dtype != UNET_F32) { set_error("unet_bn_bwd_apply: bf16 gradient needs bf16 y"); return UNET_ERR_ARG; }
   if (bn_vec_ok(C)) {
     long long b = (P * (C / 8) + 255) / 256;
     if (b > 8192) b = 8192;
-    if (dtype == UNET_BF16)
-      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<bf16>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, P, C, da,
+    if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
+      hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<bf16, bf16>), dim3((int)b), dim3(256), 0, st, P, C, (const bf16*)da,
+                         (const bf16*)y, scale, shift, relu, coef, (bf16*)dy);
+    else if (dtype == UNET_BF16)
+      hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<bf16, float>), dim3((int)b), dim3(256), 0, st, P, C, (const float*)da,
                          (const bf16*)y, scale, shift, relu, coef, (bf16*)dy);
     else
-      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<float>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, P, C, da,
+      hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<float, float>), dim3((int)b), dim3(256), 0, st, P, C, (const float*)da,
                          (const float*)y, scale, shift, relu, coef, (float*)dy);
     return check_launch("bn_bwd_apply");
   }
   const int cl = chan_lanes(C), rows = reduce_rows(P, C);
   dim3 grid(cdiv(C, cl), rows);
-  if (dtype == UNET_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, C, cl, da,
+  if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, bf16>), grid, dim3(256), 0, st, P, C, cl, (const bf16*)da,
+                       (const bf16*)y, scale, shift, relu, coef, (bf16*)dy, rows);
+  else if (dtype == UNET_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
                        (const bf16*)y, scale, shift, relu, coef, (bf16*)dy, rows);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, P, C, cl, da,
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
                        (const float*)y, scale, shift, relu, coef, (float*)dy, rows);
   return check_launch("bn_bwd_apply");
 }

@@ -64,9 +64,9 @@ _SIGS = {
                                  c_vp, c_vp, c_vp]),
     "unet_bn_eval_affine": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_vp]),
     "unet_bn_bwd_reduce_rows": (c_int, [c_ll, c_int]),
-    "unet_bn_bwd_reduce": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "unet_bn_bwd_reduce": (c_int, [c_int, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "unet_bn_bwd_finalize": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
-    "unet_bn_bwd_apply": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "unet_bn_bwd_apply": (c_int, [c_int, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
     "unet_colsum": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp]),
     "unet_gate_psi_rows": (c_int, [c_ll]),
     "unet_gate_psi": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

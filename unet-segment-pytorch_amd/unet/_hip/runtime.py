@@ -175,7 +175,8 @@ def fill_zero(t: torch.Tensor) -> None:
 class Act:
     """A stored NHWC tensor plus the per-channel affine (+ReLU) that makes it the reference's
     activation (relu(bn(y)) of a DoubleConv half, or the identity for a materialised input).
-    `grad` is the fp32 NHWC gradient w.r.t. that activation, accumulated by its consumers."""
+    `grad` is the NHWC gradient w.r.t. that activation, accumulated by its consumers: fp32, or bf16
+    for a single-consumer activation in bf16 mode (`grad_single`)."""
 
     __slots__ = ("data", "N", "H", "W", "C", "ab", "relu", "mean", "invstd", "grad", "_grad_init", "keep")
 
@@ -211,6 +212,14 @@ class Act:
         acc = self._grad_init
         self._grad_init = True
         return self.grad, int(acc)
+
+    def grad_single(self, dtype: torch.dtype) -> torch.Tensor:
+        """Buffer for the one and only contribution to this activation's gradient (stored, not
+        accumulated): a DoubleConv's middle activation, whose only consumer is the second conv."""
+        assert self.grad is None and not self._grad_init, "activation has another gradient contribution"
+        self.grad = torch.empty(self.N, self.H, self.W, self.C, dtype=dtype, device=self.data.device)
+        self._grad_init = True
+        return self.grad
 
     def grad_zeroed(self) -> torch.Tensor:
         if self.grad is None:

@@ -110,7 +110,8 @@ class ConvBN:
         assert a.has_grad(), "activation gradient missing"
         rows = L.load().unet_bn_bwd_reduce_rows(P, C)
         part = f32(2, rows, C, device=dev)
-        L.call("unet_bn_bwd_reduce", prec.code, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+        gcode = L.BF16 if a.grad.dtype == torch.bfloat16 else L.F32
+        L.call("unet_bn_bwd_reduce", prec.code, gcode, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
                int(a.relu), vp(a.mean), vp(a.invstd), vp(part), stream())
         dgamma, dbeta, coef = f32(C, device=dev), f32(C, device=dev), f32(3, C, device=dev)
         L.call("unet_bn_bwd_finalize", vp(part[0]), vp(part[1]), rows, C, P, vp(self.bn.weight), vp(a.mean),
@@ -118,7 +119,7 @@ class ConvBN:
         grads.put(self.bn.weight, dgamma)
         grads.put(self.bn.bias, dbeta)
         dy = torch.empty(a.N, a.H, a.W, C, dtype=prec.torch_dtype, device=dev)
-        L.call("unet_bn_bwd_apply", prec.code, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+        L.call("unet_bn_bwd_apply", prec.code, gcode, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
                int(a.relu), vp(coef), vp(dy), stream())
         return dy
 
@@ -150,7 +151,11 @@ class ConvBN:
         wt = self.pre_wt if self.pre_wt is not None else pack_weight(self.conv.weight, prec, transpose=True)
         self.pre_wt = None
         d = _conv_desc(prec, N, H, W, self.cout, self.cin, self.k, [_plain_src(dy)], wt)
-        if dgrad["mode"] == "pool":
+        if dgrad["mode"] == "y":
+            # op-dtype gradient, stored (the y epilogue without BN sums)
+            d.out_mode = L.OUT_Y
+            d.out = dgrad["out"].data_ptr()
+        elif dgrad["mode"] == "pool":
             d.out_mode = L.OUT_POOL_BWD
             d.out = dgrad["out"].data_ptr()
             d.pool_src = dgrad["pool_src"]
@@ -184,8 +189,14 @@ class DoubleConvStage:
 
     def backward(self, prec, grads: Grads, dgrad: Optional[dict]):
         dy2 = self.c2.bn_backward(prec, self.a2, grads)
-        g1, acc = self.a1.grad_target()
-        self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, {"mode": "f32", "out": g1, "accum": acc})
+        if prec.code == L.BF16:
+            # the middle activation has one consumer (the second conv): its gradient is written once,
+            # in bf16 (as under torch.autocast), which halves the dgrad store and the BN-backward reads
+            g1 = self.a1.grad_single(torch.bfloat16)
+            self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, {"mode": "y", "out": g1})
+        else:
+            g1, acc = self.a1.grad_target()
+            self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, {"mode": "f32", "out": g1, "accum": acc})
         del dy2
         dy1 = self.c1.bn_backward(prec, self.a1, grads)
         self.c1.conv_backward(prec, dy1, self.srcs, grads, dgrad)
