@@ -202,8 +202,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int 
     const int c = cv * 8 + j;
     sc[j] = scale[c]; sf[j] = shift[c]; A[j] = coef[c]; B[j] = coef[C + c]; Cc[j] = coef[2 * C + c];
   }
+  const int cvs = __builtin_ctz(CV);  // CV is a power of two (bn_vec_ok)
   for (; e < total; e += stride) {
-    const long long p = e / CV;
+    const long long p = e >> cvs;
     float yv[8], g[8], o[8];
     load_vec<T>(y + p * C + cv * 8, yv);
     if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);

@@ -22,10 +22,12 @@ int smallcin_rows(long long P) {
 
 bool smallcin_conv_ok(const unet_conv_desc* d) {
   return d->nsrc == 1 && d->src[0].kind == UNET_SRC_NCHW_F32 && d->Cin <= 4 && d->ksize == 3 &&
+         (double)d->N * d->H * d->W < 2147483648.0 &&
          d->out_mode == UNET_OUT_Y && (d->Cout % 8) == 0;
 }
 bool smallcin_wgrad_ok(const unet_wgrad_desc* d) {
-  return d->nsrc == 1 && d->src[0].kind == UNET_SRC_NCHW_F32 && d->Cin <= 4 && d->ksize == 3 && (d->Cout % 8) == 0;
+  return d->nsrc == 1 && d->src[0].kind == UNET_SRC_NCHW_F32 && d->Cin <= 4 && d->ksize == 3 && (d->Cout % 8) == 0 &&
+         (double)d->N * d->H * d->W < 2147483648.0;
 }
 
 // packed-weight element (co, ci, tap) of the fragment-major layout written by conv.hip pack_kernel
@@ -74,24 +76,49 @@ __global__ __launch_bounds__(256) void smallcin_fwd_kernel(const unet_conv_desc 
   float s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  // single input channel (the model's 1-channel slices): the 72 weights of this thread's 8 output
+  // channels live in registers instead of being re-read from LDS for every pixel
+  float w1[8][9];
+  if (d.Cin == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) w1[j][t] = ws[(g * 8 + j) * KK + t];
+  }
   if (pl < PPB) {
+    // pixel index math in 32 bits (host-checked P < 2^31); the column advances by PPB per step
+    unsigned q = (unsigned)(p0 + pl);
+    int xx = (int)(q % (unsigned)d.W);
+    unsigned t2 = q / (unsigned)d.W;
+    int yy = (int)(t2 % (unsigned)d.H);
+    int n = (int)(t2 / (unsigned)d.H);
     for (long long p = p0 + pl; p < p1; p += PPB) {
-      const int xx = p % d.W;
-      const long long t2 = p / d.W;
-      const int yy = t2 % d.H;
-      const long long n = t2 / d.H;
       float acc[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-      for (int ci = 0; ci < d.Cin; ++ci) {
+      if (d.Cin == 1) {
         float v[9];
-        load_taps(x, n, s.C, d.H, d.W, yy, xx, ci, v);
+        load_taps(x, n, s.C, d.H, d.W, yy, xx, 0, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float* wr = ws + (g * 8 + j) * KK + ci * 9;
+        for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int t = 0; t < 9; ++t) acc[j] += wr[t] * v[t];
+          for (int t = 0; t < 9; ++t) acc[j] += w1[j][t] * v[t];
+      } else {
+        for (int ci = 0; ci < d.Cin; ++ci) {
+          float v[9];
+          load_taps(x, n, s.C, d.H, d.W, yy, xx, ci, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float* wr = ws + (g * 8 + j) * KK + ci * 9;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) acc[j] += wr[t] * v[t];
+          }
         }
+      }
+      xx += PPB;
+      while (xx >= d.W) {
+        xx -= d.W;
+        if (++yy == d.H) { yy = 0; ++n; }
       }
       store_vec<T>((T*)d.out + p * d.Cout + g * 8, acc);
       if constexpr (sizeof(T) == 4) store_vec<T>((T*)d.out + p * d.Cout + g * 8 + 4, acc + 4);
@@ -142,11 +169,12 @@ __global__ __launch_bounds__(256) void smallcin_wgrad_kernel(const unet_wgrad_de
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[j][t] = 0.f;
       if (g < G) {
+        const unsigned q0 = (unsigned)(p0 + wave * PPW + ps);
+        int xx = (int)(q0 % (unsigned)d.W);
+        const unsigned t2 = q0 / (unsigned)d.W;
+        int yy = (int)(t2 % (unsigned)d.H);
+        int n = (int)(t2 / (unsigned)d.H);
         for (long long p = p0 + wave * PPW + ps; p < p1; p += 4 * PPW) {
-          const int xx = p % d.W;
-          const long long t2 = p / d.W;
-          const int yy = t2 % d.H;
-          const long long n = t2 / d.H;
           float v[9], gy[8];
           load_taps(x, n, s.C, d.H, d.W, yy, xx, ci, v);
           load_vec<T>(dy + p * d.Cout + g * 8, gy);
@@ -155,6 +183,11 @@ __global__ __launch_bounds__(256) void smallcin_wgrad_kernel(const unet_wgrad_de
           for (int j = 0; j < 8; ++j)
 #pragma unroll
             for (int t = 0; t < 9; ++t) acc[j][t] += gy[j] * v[t];
+          xx += 4 * PPW;
+          while (xx >= d.W) {
+            xx -= d.W;
+            if (++yy == d.H) { yy = 0; ++n; }
+          }
         }
       }
       // reduce over the PPW pixel slots of the wave (lanes with equal g0), then over the 4 waves
