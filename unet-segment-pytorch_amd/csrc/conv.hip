@@ -374,21 +374,41 @@ __global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_des
 struct ConvCfg {
   int wm, wn, ntn, raw;
   const char* name;
+  int w4;  // bf16 3x3, plain/act sources: 4-wave 8-row conv3 tile with 8-row waves (two workgroups per CU)
 };
+
+// UNET_CONV3_TILE=16 restores the 8-wave 16-row conv3 tiles (one workgroup per CU) for comparison
+static bool conv3_w4_enabled() {
+  static const int v = [] {
+    const char* e = getenv("UNET_CONV3_TILE");
+    return (e && atoi(e) == 16) ? 0 : 1;
+  }();
+  return v != 0;
+}
 
 static ConvCfg pick_cfg(const unet_conv_desc* d) {
   ConvCfg c;
   c.raw = 1;
   for (int i = 0; i < d->nsrc; ++i)
     if (d->src[i].kind == UNET_SRC_POOL_ACT || d->src[i].kind == UNET_SRC_UP_ACT) c.raw = 4;
+  c.w4 = 0;
   const long long tiles16 = (long long)d->N * cdiv(d->H, 16) * cdiv(d->W, CTW);
+  // 8-row 4-wave conv3 tiles: same 8-row x 16-px x 8-rows-per-wave MFMA work per wave as the 16-row
+  // 8-wave tile, but two independent workgroups share a CU, so one's barrier / staging / epilogue runs
+  // under the other's MFMAs
+  // (measured: faster for the y epilogue; the fp32 dgrad and pool-routing epilogues spill in the 4-wave
+  // tile and keep the 16-row one)
+  const bool w4 = conv3_w4_enabled() && d->dtype == UNET_BF16 && d->ksize == 3 && c.raw == 1 &&
+                  d->out_mode == UNET_OUT_Y;
   if (d->Cout <= 32) {
     c.wm = 2; c.wn = 2; c.ntn = 1;
   } else if (d->Cout <= 64) {
-    if (tiles16 >= 256) { c.wm = 4; c.wn = 2; c.ntn = 2; }
+    if (tiles16 >= 256 && w4) { c.wm = 2; c.wn = 2; c.ntn = 2; c.w4 = 1; }
+    else if (tiles16 >= 256) { c.wm = 4; c.wn = 2; c.ntn = 2; }
     else { c.wm = 2; c.wn = 2; c.ntn = 2; }
   } else {
-    if (c.raw == 1 && tiles16 * cdiv(d->Cout, 128) >= 256) { c.wm = 4; c.wn = 2; c.ntn = 4; }
+    if (c.raw == 1 && tiles16 * cdiv(d->Cout, 128) >= 256 && w4) { c.wm = 2; c.wn = 2; c.ntn = 4; c.w4 = 1; }
+    else if (c.raw == 1 && tiles16 * cdiv(d->Cout, 128) >= 256) { c.wm = 4; c.wn = 2; c.ntn = 4; }
     else { c.wm = 2; c.wn = 4; c.ntn = 2; }
   }
   return c;
@@ -553,6 +573,10 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
   const ConvCfg c = pick_cfg(d);
   if (conv3_eligible(d)) {
     // the (wm, wn, ntn) block tile of pick_cfg; 16-row tiles run as MI=8 waves (dispatch_conv3)
+    if (c.w4) {
+      snprintf(buf, len, "conv3_kernel<bf16,3,1,4,%d,8,1>", c.ntn / 2);
+      return 0;
+    }
     const bool mi8 = c.raw == 1 && c.wm == 4 && (c.ntn == 4 || c.ntn == 2);
     snprintf(buf, len, "conv3_kernel<bf16,3,%d,%d,%d,%d,%d>", mi8 ? 2 : c.wm, mi8 ? 4 : c.wn, mi8 ? c.ntn / 2 : c.ntn,
              mi8 ? 8 : 4, c.raw);
