@@ -173,7 +173,7 @@ def test_conv_dgrad_split_and_pool(prec, shape):
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])
 @pytest.mark.parametrize("shape", [(2, 16, 16, 64, 64), (1, 24, 40, 32, 128), (2, 40, 36, 128, 256),
-                                   (4, 32, 32, 96, 64)])
+                                   (4, 32, 32, 96, 64), (4, 128, 128, 64, 64)])   # last: >32 split-K slabs
 @pytest.mark.parametrize("k", [3, 1])
 @pytest.mark.parametrize("kind", ["act", "pool"])
 def test_conv_wgrad(prec, shape, k, kind):

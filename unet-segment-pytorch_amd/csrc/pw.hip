@@ -374,6 +374,18 @@ __global__ void pw_slab_reduce_kernel(const float* ws, int splits, int per, long
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
+// dw (+)= Σ_s ws[s] over `splits` slabs of `total` floats (total % 4 == 0) in two fixed-order passes
+// through PW_RG partial slabs at `scratch` (PW_RG * total floats)
+int slab_reduce_two_pass(const float* ws, int splits, long long total, float* scratch, float* dw, int accum,
+                         hipStream_t st) {
+  const long long total4 = total / 4;
+  const int per = cdiv(splits, PW_RG), groups = cdiv(splits, per);
+  hipLaunchKernelGGL(pw_slab_reduce_kernel, dim3(cdiv(total4, 256), groups), dim3(256), 0, st, ws, splits, per, total4,
+                     scratch, 0);
+  hipLaunchKernelGGL(pw_slab_reduce_kernel, dim3(cdiv(total4, 256), 1), dim3(256), 0, st, (const float*)scratch, groups,
+                     groups, total4, dw, accum);
+  return check_launch("slab_reduce");
+}
 static bool pw_src_ok(const unet_src& s, int C) {
   return (s.kind == UNET_SRC_PLAIN || s.kind == UNET_SRC_ACT) && s.C == C && !(s.gate_p && s.kind != UNET_SRC_ACT);
 }
@@ -472,15 +484,9 @@ int pw_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
   else e = p.mb == 4 ? launch_pww<1, 4>(d, p, st) : p.mb == 2 ? launch_pww<1, 2>(d, p, st) : launch_pww<1, 1>(d, p, st);
   if (e) return e;
   // slabs -> PW_RG partial slabs (written after the split slabs in the workspace) -> dw
-  const long long total = (long long)d->Cout * d->Cin, total4 = total / 4;
-  const float* ws = (const float*)d->workspace;
-  float* part = (float*)d->workspace + (size_t)p.splits * total;
-  const int per = cdiv(p.splits, PW_RG), groups = cdiv(p.splits, per);
-  hipLaunchKernelGGL(pw_slab_reduce_kernel, dim3(cdiv(total4, 256), groups), dim3(256), 0, st, ws, p.splits, per, total4,
-                     part, 0);
-  hipLaunchKernelGGL(pw_slab_reduce_kernel, dim3(cdiv(total4, 256), 1), dim3(256), 0, st, part, groups, groups, total4,
-                     d->dw, d->accum);
-  return check_launch("pw_slab_reduce");
+  const long long total = (long long)d->Cout * d->Cin;
+  return slab_reduce_two_pass((const float*)d->workspace, p.splits, total,
+                              (float*)d->workspace + (size_t)p.splits * total, d->dw, d->accum, st);
 }
 
 }  // namespace unet

@@ -18,6 +18,9 @@
 namespace unet {
 
 constexpr int W2_TH = 8, W2_TW = 16, W2_BM = 128;
+constexpr int W2_RG = 32, W2_RG_MIN = 32;  // two-pass slab reduction above W2_RG_MIN splits
+int slab_reduce_two_pass(const float* ws, int splits, long long total, float* scratch, float* dw, int accum,
+                         hipStream_t st);  // pw.hip (W2_RG == PW_RG partial slabs)
 
 __device__ __forceinline__ bf16x8 tr8(const bf16* r0, const bf16* r1) {
   const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r0));
@@ -300,7 +303,8 @@ W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   if (s < 1) s = 1;
   p.per_split = cdiv(p.mtiles, s);
   p.splits = cdiv(p.mtiles, p.per_split);
-  p.ws_bytes = slab * p.splits;
+  // + room for the partial slabs of the two-pass reduction (many splits of a small weight tensor)
+  p.ws_bytes = slab * (p.splits + (p.splits > W2_RG_MIN ? W2_RG : 0));
   return p;
 }
 
@@ -330,8 +334,14 @@ int launch_wgrad2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
   if (d->ksize == 3) e = p.raw == 4 ? launch_w2_cfg<3, 4>(d, p, st) : launch_w2_cfg<3, 1>(d, p, st);
   else e = p.raw == 4 ? launch_w2_cfg<1, 4>(d, p, st) : launch_w2_cfg<1, 1>(d, p, st);
   if (e) return e;
-  return wgrad_reduce2_launch((const float*)d->workspace, p.splits, (long long)d->Cout * d->Cin * d->ksize * d->ksize,
-                              d->dw, d->accum, st);
+  const long long total = (long long)d->Cout * d->Cin * d->ksize * d->ksize;
+  if (p.splits > W2_RG_MIN && (total & 3) == 0) {
+    // two fixed-order passes (splits -> W2_RG groups -> 1): one serial loop of hundreds of slabs per
+    // 16-byte column would leave the reduction latency-bound for small weights (e.g. 64x64x3x3)
+    return slab_reduce_two_pass((const float*)d->workspace, p.splits, total,
+                                (float*)d->workspace + (size_t)p.splits * total, d->dw, d->accum, st);
+  }
+  return wgrad_reduce2_launch((const float*)d->workspace, p.splits, total, d->dw, d->accum, st);
 }
 
 // entry points used by wgrad.hip (which keeps the generic kernel for fp32 / odd channel counts)
