@@ -409,6 +409,9 @@ static ConvCfg pick_cfg(const unet_conv_desc* d) {
   } else {
     if (c.raw == 1 && tiles16 * cdiv(d->Cout, 128) >= 256 && w4) { c.wm = 2; c.wn = 2; c.ntn = 4; c.w4 = 1; }
     else if (c.raw == 1 && tiles16 * cdiv(d->Cout, 128) >= 256) { c.wm = 4; c.wn = 2; c.ntn = 4; }
+    else if ((long long)d->N * cdiv(d->H, 8) * cdiv(d->W, CTW) * cdiv(d->Cout, 128) < 256) {
+      c.wm = 2; c.wn = 2; c.ntn = 2;  // small maps (32^2 x bs4): 64-channel tiles, twice the workgroups
+    }
     else { c.wm = 2; c.wn = 4; c.ntn = 2; }
   }
   return c;
