@@ -596,15 +596,21 @@ class NetworkPlan:
         gl = gouts[0]
         if gl is None:
             gl = torch.zeros(self.x.shape[0], self.outc.k, self.x.shape[2], self.x.shape[3], device=self.x.device)
+        # data-parallel gradient averaging overlapped with the remaining stages (unet.utils.distributed)
+        sync = getattr(self.model, "_grad_sync", None)
+        hook = sync.stage_done if sync is not None else (lambda g: None)
         self.outc.backward(prec, gl, grads)
         if self.with_ds:
             for head, g in zip(self.heads, gouts[1:]):
                 if g is not None:
                     head.backward(prec, g, grads)
+        hook(grads)
         for u in reversed(self.ups):
             u.backward(prec, grads)
+            hook(grads)
         for d in reversed(self.downs):
             d.backward(prec, grads)
+            hook(grads)
         dx = None
         if self.need_dx:
             x = self.x
@@ -615,6 +621,8 @@ class NetworkPlan:
             dx = grad_nhwc_to_nchw(gx)
         else:
             self.inc.backward(prec, grads, None)
+        if sync is not None:
+            sync.finish(grads)
         return dx
 
 
