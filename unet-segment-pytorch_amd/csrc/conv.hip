@@ -121,6 +121,48 @@ __device__ __forceinline__ void conv_epilogue(const unet_conv_desc& d, f32x4 (&a
         }
       }
     }
+  } else if (is(UNET_OUT_POOL_BWD) && d.pool_code && (d.Cout % 4) == 0) {
+    // max-pool backward through the argmax codes of unet_materialize_pool: the row is transposed through
+    // a wave-private LDS slice as in the fp32 path, so a lane owns 4 consecutive channels of one pooled
+    // pixel (one 4-byte code load) and adds each channel into the 2x2 source position it selected: all four
+    // positions are read-modify-written as 16-byte accesses with per-channel selects (no divergence; the
+    // cache lines are touched either way), instead of 4-byte scattered accesses per channel
+    const unet_src& ps = d.pool_src;
+    float* da = (float*)d.out;
+    constexpr int SW = NTN * 16 + 4;
+    float* stg = reinterpret_cast<float*>(lds) + (wm * WN + wn) * 16 * SW;
+#pragma unroll MI
+    for (int i = 0; i < MI; ++i) {
+      const int oh = h0 + wm * MI + i;
+#pragma unroll NTN
+      for (int j = 0; j < NTN; ++j)
+#pragma unroll 4
+        for (int r = 0; r < 4; ++r) stg[(4 * (lane >> 4) + r) * SW + j * 16 + (lane & 15)] = acc[i][j][r];
+#pragma unroll
+      for (int k = 0; k < NTN; ++k) {
+        const int f = lane + 64 * k;
+        const int px = f / (4 * NTN), c4 = f % (4 * NTN);
+        const float4 v = *reinterpret_cast<const float4*>(stg + px * SW + c4 * 4);
+        const int ow = w0 + px, co = co0 + wn * NTN * 16 + c4 * 4;
+        if (oh < d.H && ow < d.W && co < d.Cout) {
+          const long long pix = (n * d.H + oh) * (long long)d.W + ow;
+          const unsigned code = *reinterpret_cast<const unsigned*>(d.pool_code + pix * d.Cout + co);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const bool s0 = (code & 0xffu) == (unsigned)q, s1 = ((code >> 8) & 0xffu) == (unsigned)q;
+            const bool s2 = ((code >> 16) & 0xffu) == (unsigned)q, s3 = (code >> 24) == (unsigned)q;
+            const long long sp = (n * ps.H + 2 * oh + (q >> 1)) * (long long)ps.W + 2 * ow + (q & 1);
+            float4* p = reinterpret_cast<float4*>(da + sp * d.Cout + co);
+            float4 a = *p;
+            a.x = s0 ? a.x + v.x : a.x;
+            a.y = s1 ? a.y + v.y : a.y;
+            a.z = s2 ? a.z + v.z : a.z;
+            a.w = s3 ? a.w + v.w : a.w;
+            *p = a;
+          }
+        }
+      }
+    }
   } else if (is(UNET_OUT_F32)) {
     float* o1 = (float*)d.out;
     float* o2 = (float*)d.out2;

@@ -12,6 +12,7 @@ namespace unet {
 
 constexpr int SC_ROWS_MAX = 1024;
 constexpr int SC_MAXK = 36;  // 9 taps x 4 channels
+constexpr int SC_U = 4;      // pixels per trip of the 1-channel forward loop
 
 int smallcin_rows(long long P) {
   long long r = (P + 1023) / 1024;
@@ -85,7 +86,40 @@ __global__ __launch_bounds__(256) void smallcin_fwd_kernel(const unet_conv_desc 
 #pragma unroll
       for (int t = 0; t < 9; ++t) w1[j][t] = ws[(g * 8 + j) * KK + t];
   }
-  if (pl < PPB) {
+  if (pl < PPB && d.Cin == 1) {
+    // 1-channel input: SC_U pixels per trip with all their tap loads issued before the FMAs (the loop
+    // is load-latency bound at 4 waves per SIMD).  Pixels and stats keep the one-pixel loop's order.
+    const int per_i = (int)(p1 - p0);
+    for (int b = pl; b < per_i; b += SC_U * PPB) {
+      float v[SC_U][9];
+#pragma unroll
+      for (int u = 0; u < SC_U; ++u) {
+        const int lp = b + u * PPB;
+        const unsigned q = (unsigned)(p0 + (lp < per_i ? lp : per_i - 1));
+        const int xx = (int)(q % (unsigned)d.W);
+        const unsigned t2 = q / (unsigned)d.W;
+        load_taps(x, (int)(t2 / (unsigned)d.H), s.C, d.H, d.W, (int)(t2 % (unsigned)d.H), xx, 0, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < SC_U; ++u) {
+        const int lp = b + u * PPB;
+        if (lp < per_i) {
+          float acc[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            acc[j] = 0.f;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) acc[j] += w1[j][t] * v[u][t];
+          }
+          const long long p = p0 + lp;
+          store_vec<T>((T*)d.out + p * d.Cout + g * 8, acc);
+          if constexpr (sizeof(T) == 4) store_vec<T>((T*)d.out + p * d.Cout + g * 8 + 4, acc + 4);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s1[j] += acc[j]; s2[j] += acc[j] * acc[j]; }
+        }
+      }
+    }
+  } else if (pl < PPB) {
     // pixel index math in 32 bits (host-checked P < 2^31); the column advances by PPB per step
     unsigned q = (unsigned)(p0 + pl);
     int xx = (int)(q % (unsigned)d.W);
@@ -96,23 +130,14 @@ __global__ __launch_bounds__(256) void smallcin_fwd_kernel(const unet_conv_desc 
       float acc[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-      if (d.Cin == 1) {
+      for (int ci = 0; ci < d.Cin; ++ci) {
         float v[9];
-        load_taps(x, n, s.C, d.H, d.W, yy, xx, 0, v);
+        load_taps(x, n, s.C, d.H, d.W, yy, xx, ci, v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < 8; ++j) {
+          const float* wr = ws + (g * 8 + j) * KK + ci * 9;
 #pragma unroll
-          for (int t = 0; t < 9; ++t) acc[j] += w1[j][t] * v[t];
-      } else {
-        for (int ci = 0; ci < d.Cin; ++ci) {
-          float v[9];
-          load_taps(x, n, s.C, d.H, d.W, yy, xx, ci, v);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float* wr = ws + (g * 8 + j) * KK + ci * 9;
-#pragma unroll
-            for (int t = 0; t < 9; ++t) acc[j] += wr[t] * v[t];
-          }
+          for (int t = 0; t < 9; ++t) acc[j] += wr[t] * v[t];
         }
       }
       xx += PPB;
