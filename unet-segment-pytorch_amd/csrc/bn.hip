@@ -28,11 +28,30 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
   return r;
 }
 
+
+// the (sum, sum) pair of a block in one LDS round (fixed order: waves in index order)
+__device__ __forceinline__ void block_sum2_d(double& a, double& b, double* sh) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+  if ((tid & 63) == 0) { sh[2 * (tid >> 6)] = a; sh[2 * (tid >> 6) + 1] = b; }
+  __syncthreads();
+  a = 0; b = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { a += sh[2 * w]; b += sh[2 * w + 1]; }
+}
+
+// finalize blocks: one trip of 4 loads per thread for up to 4096 partial rows (the kernels are a few
+// dependent memory round trips long; fewer trips = shorter kernels)
+static inline int fin_threads(int rows) {
+  int t = ((rows + 3) / 4 + 63) / 64 * 64;
+  return t < 64 ? 64 : (t > 1024 ? 1024 : t);
+}
+
 // one block per channel
 __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long long count, const float* gamma,
                                    const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
                                    float eps, float* mean, float* invstd, float* scale, float* shift) {
-  __shared__ double sh[16];
+  __shared__ double sh2[32];
   const int c = blockIdx.x;
   double s = 0, ss = 0;
   const float* s0 = stats + (size_t)c * rows;         // [2][C][rows]: contiguous over r
@@ -51,8 +70,7 @@ __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long lon
     s += s0[r];
     ss += s1[r];
   }
-  s = block_sum_d(s, sh);
-  ss = block_sum_d(ss, sh);
+  block_sum2_d(s, ss, sh2);
   if (threadIdx.x == 0) {
     const double m = s / (double)count;
     double var = ss / (double)count - m * m;
@@ -239,7 +257,7 @@ static inline int reduce_rows_vec(long long P, int C) {
 __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
                                        const float* gamma, const float* mean, const float* invstd, float* dgamma,
                                        float* dbeta, int accum, float* coef) {
-  __shared__ double sh[16];
+  __shared__ double sh2[32];
   const int c = blockIdx.x;
   double a = 0, b = 0;
   const int B = blockDim.x;
@@ -256,8 +274,7 @@ __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, 
     a += sum_g[(size_t)r * C + c];
     b += sum_gx[(size_t)r * C + c];
   }
-  a = block_sum_d(a, sh);
-  b = block_sum_d(b, sh);
+  block_sum2_d(a, b, sh2);
   if (threadIdx.x == 0) {
     if (dbeta) dbeta[c] = accum ? dbeta[c] + (float)a : (float)a;
     if (dgamma) dgamma[c] = accum ? dgamma[c] + (float)b : (float)b;
@@ -313,7 +330,7 @@ int unet_bn_finalize(const float* stats, int rows, int C, long long count, const
     set_error("unet_bn_finalize: bad args");
     return UNET_ERR_ARG;
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, stats, rows, C, count, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(fin_threads(rows)), 0, (hipStream_t)stream, stats, rows, C, count, gamma,
                      beta, running_mean, running_var, nbt, momentum, eps, mean, invstd, scale, shift);
   return check_launch("bn_finalize");
 }
@@ -362,7 +379,7 @@ int unet_bn_bwd_reduce(int dtype, int da_dtype, long long P, int C, const void* 
 int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int C, long long count, const float* gamma,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, int accum, float* coef,
                          void* stream) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, sum_g, sum_gx, rows, C, count,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(fin_threads(rows)), 0, (hipStream_t)stream, sum_g, sum_gx, rows, C, count,
                      gamma, mean, invstd, dgamma, dbeta, accum, coef);
   return check_launch("bn_bwd_finalize");
 }
