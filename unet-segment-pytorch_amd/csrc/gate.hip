@@ -177,39 +177,56 @@ __global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* dx
   const long long per = (P + rows - 1) / rows;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
   float s1 = 0.f, s2 = 0.f;
-  for (long long q = p0 + wave * ppw + lane / G; q < p1; q += (long long)nw * ppw) {
-    float d[8], y[8];
-    load_vec<float>(dxs + q * Cx + c0, d);
-    load_vec<float>(dxs + q * Cx + c0 + 4, d + 4);
-    load8<T>(yx + q * Cx + c0, y);
-    const float pv = pp[q];
-    const float sg = sigmoidf_(pv * pa + pb);
-    float ds = 0.f;
+  // two pixels per trip with every load issued before the stores (the stores to dx may alias the loads
+  // as far as the compiler knows, so a one-pixel loop serialises a full memory round trip per pixel);
+  // s1 / s2 keep the one-pixel loop's pixel order
+  const long long S = (long long)nw * ppw;
+  for (long long q = p0 + wave * ppw + lane / G; q < p1; q += 2 * S) {
+    float d[2][8], y[2][8], g[2][8], pv[2];
+    bool ok[2];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float xv = y[j] * sc[j] + sf[j];
-      if (relu) xv = fmaxf(xv, 0.f);
-      ds += d[j] * xv;
+    for (int u = 0; u < 2; ++u) {
+      ok[u] = q + u * S < p1;
+      const long long qq = ok[u] ? q + u * S : q;
+      load_vec<float>(dxs + qq * Cx + c0, d[u]);
+      load_vec<float>(dxs + qq * Cx + c0 + 4, d[u] + 4);
+      load8<T>(yx + qq * Cx + c0, y[u]);
+      pv[u] = pp[qq];
+      if (dx_accum) {
+        load_vec<float>(dx + qq * Cx + c0, g[u]);
+        load_vec<float>(dx + qq * Cx + c0 + 4, g[u] + 4);
+      }
     }
-    float* o = dx + q * Cx + c0;
-    float g[8];
-    if (dx_accum) {
-      load_vec<float>(o, g);
-      load_vec<float>(o + 4, g + 4);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] += d[j] * sg;
-    } else {
+    for (int u = 0; u < 2; ++u) {
+      const float sg = sigmoidf_(pv[u] * pa + pb);
+      float ds = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = d[j] * sg;
-    }
-    store_vec<float>(o, g);
-    store_vec<float>(o + 4, g + 4);
-    ds = group_sum(ds, G);
-    if (sub == 0) {
-      const float dqv = ds * sg * (1.f - sg);
-      dq[q] = dqv;
-      s1 += dqv;
-      s2 += dqv * (pv - pm) * pi;
+      for (int j = 0; j < 8; ++j) {
+        float xv = y[u][j] * sc[j] + sf[j];
+        if (relu) xv = fmaxf(xv, 0.f);
+        ds += d[u][j] * xv;
+      }
+      if (dx_accum) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[u][j] += d[u][j] * sg;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[u][j] = d[u][j] * sg;
+      }
+      ds = group_sum(ds, G);
+      if (ok[u]) {
+        const long long qq = q + u * S;
+        float* o = dx + qq * Cx + c0;
+        store_vec<float>(o, g[u]);
+        store_vec<float>(o + 4, g[u] + 4);
+        if (sub == 0) {
+          const float dqv = ds * sg * (1.f - sg);
+          dq[qq] = dqv;
+          s1 += dqv;
+          s2 += dqv * (pv[u] - pm) * pi;
+        }
+      }
     }
   }
   s1 = block_sum_f(s1, sh);
