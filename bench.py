@@ -179,6 +179,29 @@ def main():
     elapsed = max_over_ranks(elapsed, dev)
     ps = probe.summary()
 
+    # SURVEY §8(d) also asks for the rate without the optimizer: the same fwd + loss + bwd (+ gradient
+    # averaging) micro-steps, gradients dropped instead of clip + AdamW (reported beside `value`)
+    def fwd_bwd():
+        for k in range(args.accum):
+            last = k == args.accum - 1
+            ctx = net.no_sync() if (world > 1 and not last) else contextlib.nullcontext()
+            with ctx:
+                l = crit(net(x), t)
+                (l / args.accum if args.accum > 1 else l).backward()
+        opt.zero_grad(set_to_none=True)
+
+    fwd_bwd()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        fwd_bwd()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el_nb = max_over_ranks(time.perf_counter() - t1, dev)
+
     images = world * args.batch * args.accum * args.steps
     value = images / elapsed
     peak = MFMA_PEAK_TFLOPS[args.precision]
@@ -208,6 +231,9 @@ def main():
                      "launches": ps["launches"], "avg_us": round(ps["avg_us"], 2) if ps["avg_us"] else None,
                      "flops_per_launch": round(ps["flops"] / ps["launches"]) if ps["launches"] else None},
         "final_loss": round(float(loss.detach()), 5),
+        "without_optimizer": {"value": round(world * args.batch * args.accum * args.steps / el_nb, 3),
+                              "ms_per_step": round(el_nb / args.steps * 1e3, 3),
+                              "note": "fwd+DiceBCE+bwd (+grad averaging), no clip/AdamW"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.model, args.size, args.cpu_batch, args.cpu_iters)
