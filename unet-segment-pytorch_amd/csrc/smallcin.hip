@@ -86,7 +86,58 @@ __global__ __launch_bounds__(256) void smallcin_fwd_kernel(const unet_conv_desc 
 #pragma unroll
       for (int t = 0; t < 9; ++t) w1[j][t] = ws[(g * 8 + j) * KK + t];
   }
-  if (pl < PPB && d.Cin == 1) {
+  if (pl < PPB && d.Cin == 1 && (d.W % 2) == 0 && (per % 2) == 0) {
+    // 1-channel input, two horizontally adjacent pixels per lane and trip: their 3x4 tap window is 12
+    // loads instead of 18, the index / bounds math is shared, and the two accumulators form one packed
+    // fp32 pair (the kernel is VALU-issue bound, profiles/r01_smallcin_pmc.txt)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const int per_i = (int)(p1 - p0);
+    const long long plane = (long long)d.H * d.W;
+    for (int b = 2 * pl; b < per_i; b += 2 * PPB) {
+      const unsigned q = (unsigned)(p0 + b);
+      const int xx = (int)(q % (unsigned)d.W);
+      const unsigned t2 = q / (unsigned)d.W;
+      const int yy = (int)(t2 % (unsigned)d.H), n = (int)(t2 / (unsigned)d.H);
+      const float* xn = x + (long long)n * s.C * plane;
+      float v[3][4];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int y2 = yy + r - 1;
+        const bool rok = y2 >= 0 && y2 < d.H;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int x2 = xx + c - 1;
+          v[r][c] = (rok && x2 >= 0 && x2 < d.W) ? xn[(long long)y2 * d.W + x2] : 0.f;
+        }
+      }
+      f2 acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[j] = f2{0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const f2 tv = {v[t / 3][t % 3], v[t / 3][t % 3 + 1]};
+          acc[j] += f2{w1[j][t], w1[j][t]} * tv;
+        }
+      }
+      float a0[8], a1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a0[j] = acc[j].x; a1[j] = acc[j].y; }
+      const long long p = p0 + b;
+      T* o = (T*)d.out + p * d.Cout + g * 8;
+      store_vec<T>(o, a0);
+      store_vec<T>(o + d.Cout, a1);
+      if constexpr (sizeof(T) == 4) {
+        store_vec<T>(o + 4, a0 + 4);
+        store_vec<T>(o + d.Cout + 4, a1 + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += a0[j]; s2[j] += a0[j] * a0[j];
+        s1[j] += a1[j]; s2[j] += a1[j] * a1[j];
+      }
+    }
+  } else if (pl < PPB && d.Cin == 1) {
     // 1-channel input: SC_U pixels per trip with all their tap loads issued before the FMAs (the loop
     // is load-latency bound at 4 waves per SIMD).  Pixels and stats keep the one-pixel loop's order.
     const int per_i = (int)(p1 - p0);
