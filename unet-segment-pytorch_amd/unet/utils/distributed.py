@@ -2,7 +2,7 @@
 
 The reference trains data-parallel by batch (scripts/train.py:133-143 gradient accumulation; the
 multi-GPU row of BASELINE.json wraps the model in DDP).  Under torch DDP our whole-network backward is
-ONE autograd node, so every gradient becomes ready at the same instant and the ~140 MB all-reduce runs
+ONE autograd node, so every gradient becomes ready at the same instant and the ~70 MB all-reduce runs
 after the last weight gradient, fully exposed.  `OverlappedGradSync` instead receives a callback from
 `NetworkPlan.backward` after every stage (outc, up4 .. up1, down4 .. down1, inc): the gradients that
 stage just produced are packed into a flat bucket and averaged with an async all-reduce (RCCL on ROCm,
@@ -41,7 +41,6 @@ class OverlappedGradSync:
         self.cap = int(bucket_cap_mb * (1 << 20))
         self.params = [p for p in model.parameters() if p.requires_grad]
         self._pid = {id(p): i for i, p in enumerate(self.params)}
-        self.avg_op = dist.ReduceOp.AVG if dist.get_backend(process_group) == "nccl" else None
         self.enabled = True
         self._reset()
         with torch.no_grad():
@@ -93,11 +92,9 @@ class OverlappedGradSync:
             if p.grad is not None:          # locally accumulated micro-batches (no_sync)
                 flat[off:off + n].add_(p.grad.reshape(-1))
             off += n
-        if self.avg_op is not None:
-            work = dist.all_reduce(flat, op=self.avg_op, group=self.pg, async_op=True)
-        else:
-            flat.div_(self.world)
-            work = dist.all_reduce(flat, group=self.pg, async_op=True)
+        # divide, then SUM: DDP's own default (and every backend has SUM; gloo has no AVG)
+        flat.div_(self.world)
+        work = dist.all_reduce(flat, group=self.pg, async_op=True)
         self._buckets.append((flat, ps, work))
 
     def finish(self, grads: Dict[torch.nn.Parameter, torch.Tensor]):
