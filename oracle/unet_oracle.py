@@ -144,7 +144,7 @@ def dice_loss(z: torch.Tensor, t: torch.Tensor, smooth: float = 1.0, ignore_back
     """DiceLoss.forward — loss.py:45-85."""
     c = z.shape[1]
     pr = F.softmax(z, dim=1)
-    oh = F.one_hot(t, num_classes=c).permute(0, 3, 1, 2).float()
+    oh = F.one_hot(t, num_classes=c).permute(0, 3, 1, 2).to(z.dtype)
     inter = (pr * oh).sum(dim=(2, 3))
     union = pr.sum(dim=(2, 3)) + oh.sum(dim=(2, 3))
     d = (2.0 * inter + smooth) / (union + smooth)
@@ -166,8 +166,8 @@ def balanced_ce_loss(z: torch.Tensor, t: torch.Tensor, class_weight: float = 0.5
     for i in range(n):
         tm = t[i] == 1
         bm = t[i] == 0
-        nt = tm.sum().float() + smooth
-        nb = bm.sum().float() + smooth
+        nt = tm.sum().to(z.dtype) + smooth
+        nb = bm.sum().to(z.dtype) + smooth
         w[i][tm] = class_weight / nt
         w[i][bm] = (1 - class_weight) / nb
     return (ce * w).sum() / n

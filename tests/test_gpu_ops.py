@@ -448,3 +448,196 @@ def test_upsample_bwd(geo, accum):
            g.data_ptr(), dx.data_ptr(), accum, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert ((dx - 1.5 * accum) - ref).abs().max() <= 1e-5 * (1 + ref.abs().max())
+
+
+# ------------------------------------------------------------------------------------------------
+# The conv3 instantiations the benchmark runs (csrc/conv.hip pick_cfg: tiles16 = N*ceil(H/16)*ceil(W/16)
+# >= 256 selects the 4-wave w4 tiles for the y epilogue and the 8-wave MI=8 tiles for the fp32 dgrad and
+# pool-routing epilogues).  Bench-sized maps, so that M tiles outnumber the persistent grid and every
+# workgroup runs the multi-tile loop (next tile staged during the last chunk).  Reference: torch fp32
+# conv on the same bf16-rounded operands; gates: rel-L2 <= 4e-3 (bf16 output rounding is ~1e-3) and
+# max-abs <= 2e-2 * (1 + max|ref|).
+# ------------------------------------------------------------------------------------------------
+
+def _variant(d):
+    import ctypes
+    buf = ctypes.create_string_buffer(128)
+    _lib().load().unet_conv_variant(d, buf, 128)
+    return buf.value.decode()
+
+
+def _close_bf16(got, ref, what):
+    got, ref = got.double(), ref.double()
+    rel = float((got - ref).norm() / (ref.norm() + 1e-30))
+    mx = float((got - ref).abs().max())
+    assert rel <= 4e-3, (what, rel)
+    assert mx <= 2e-2 * (1 + float(ref.abs().max())), (what, mx)
+
+
+def _persistent(N, H, W, TH, cout, BN, w4):
+    """M tiles per workgroup of launch_conv3's grid (> 1: the persistent multi-tile loop runs)."""
+    mt = N * ((H + TH - 1) // TH) * ((W + 15) // 16)
+    gy = (cout + BN - 1) // BN
+    gx = min(mt, ((512 if w4 else 256) + gy - 1) // gy)
+    return mt / gx
+
+
+# (N, H, W, Cin, Cout, expected variant) — forward / y epilogue (+ BN partial sums)
+Y_BENCH = [
+    (4, 512, 512, 64, 64, "conv3_kernel<bf16,3,1,4,1,8,1>"),     # inc.3 / up4.conv.3
+    (4, 256, 256, 64, 128, "conv3_kernel<bf16,3,1,4,2,8,1>"),    # down1.0
+    (4, 256, 256, 128, 128, "conv3_kernel<bf16,3,1,4,2,8,1>"),   # down1.3
+    (4, 128, 128, 256, 256, "conv3_kernel<bf16,3,1,4,2,8,1>"),   # down2.3
+    (3, 200, 328, 64, 128, "conv3_kernel<bf16,3,1,4,2,8,1>"),    # partial tiles in both directions
+]
+
+
+@pytest.mark.parametrize("shape", Y_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
+@pytest.mark.parametrize("stats", [True, False])
+def test_conv3_bench_tiles_y(shape, stats):
+    L = _lib()
+    N, H, W, cin, cout, want = shape
+    dt = torch.bfloat16
+    torch.manual_seed(11)
+    y = _rand(N, H, W, cin, dt=dt)
+    ab = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2])
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
+    out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
+    L.load()
+    kw = {"out": out.data_ptr()}
+    st = None
+    if stats:
+        d0 = L.ConvDesc()
+        d0.dtype, d0.N, d0.H, d0.W, d0.Cin, d0.Cout, d0.ksize, d0.nsrc = L.BF16, N, H, W, cin, cout, 3, 1
+        d0.src[0] = _act_src(y, ab)
+        rows = L.load().unet_conv_stats_rows(d0)
+        st = torch.empty(2, cout, rows, device="cuda")
+        kw["stats"] = st.data_ptr()
+    d = _conv("bf16", [_act_src(y, ab)], N, H, W, cin, w, 3, L.OUT_Y, **kw)
+    assert _variant(d) == want, _variant(d)
+    assert _persistent(N, H, W, 8, cout, 64 if cout <= 64 else 128, True) > 1
+    x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2)
+    ref = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)
+    _close_bf16(out.float(), ref, "y")
+    if stats:
+        r = ref.double().reshape(-1, cout)
+        s = st.double().sum(-1)
+        # the sums come from the fp32 accumulators (before bf16 rounding of y)
+        assert ((s[0] - r.sum(0)).abs() <= 1e-3 * r.abs().sum(0) + 1e-2).all()
+        assert ((s[1] - (r * r).sum(0)).abs() <= 1e-2 * (r * r).sum(0) + 1e-2).all()
+
+
+# dgrad of a forward conv cin -> cout: dy[cout] -> dx[cin] (the dgrad conv has Cout = cin)
+DGRAD_BENCH = [
+    (4, 512, 512, 128, 64, "conv3_kernel<bf16,3,2,4,2,8,1>"),    # up4.conv.0 dgrad, split skip / up
+    (4, 256, 256, 256, 128, "conv3_kernel<bf16,3,2,4,2,8,1>"),   # up3.conv.0 dgrad
+    (4, 512, 512, 64, 64, "conv3_kernel<bf16,3,2,4,1,8,1>"),
+    (3, 200, 328, 128, 64, "conv3_kernel<bf16,3,2,4,2,8,1>"),
+]
+
+
+@pytest.mark.parametrize("shape", DGRAD_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
+def test_conv3_bench_tiles_dgrad_f32(shape):
+    L = _lib()
+    N, H, W, cin, cout, want = shape
+    dt = torch.bfloat16
+    torch.manual_seed(12)
+    dy = _rand(N, H, W, cout, dt=dt)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    split = cin // 2
+    o1 = torch.full((N, H, W, split), 0.5, device="cuda")
+    o2 = torch.full((N, H, W, cin - split), float("nan"), device="cuda")
+    d = _conv("bf16", [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
+              split=split, accum=1, accum2=0)
+    assert _variant(d) == want, _variant(d)
+    assert _persistent(N, H, W, 16, cin, 128 if cin > 64 else 64, False) > 1
+    got = torch.cat([o1 - 0.5, o2], -1)
+    _close_bf16(got, ref, "dgrad f32")
+
+
+@pytest.mark.parametrize("shape", [(4, 512, 512, 64, 64), (4, 256, 256, 128, 128), (3, 200, 328, 64, 64)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv3_bench_tiles_dgrad_y(shape):
+    """bf16 gradient of a DoubleConv's middle activation (the y epilogue without BN sums)."""
+    L = _lib()
+    N, H, W, cin, cout = shape
+    dt = torch.bfloat16
+    torch.manual_seed(13)
+    dy = _rand(N, H, W, cout, dt=dt)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    out = torch.empty(N, H, W, cin, dtype=dt, device="cuda")
+    d = _conv("bf16", [src], N, H, W, cout, w, 3, L.OUT_Y, transpose=True, out=out.data_ptr())
+    assert _variant(d).startswith("conv3_kernel<bf16,3,1,4,"), _variant(d)
+    _close_bf16(out.float(), ref, "dgrad y")
+
+
+# pool-routed dgrad: dy at the pooled map -> dx into the 2x map through the recorded argmax
+POOL_BENCH = [
+    (4, 256, 256, 64, 128, "conv3_kernel<bf16,3,2,4,1,8,1>"),    # down1.0 dgrad -> inc output (512^2)
+    (4, 128, 128, 128, 256, "conv3_kernel<bf16,3,2,4,2,8,1>"),   # down2.0 dgrad -> down1 output
+    (3, 130, 166, 64, 128, "conv3_kernel<bf16,3,2,4,1,8,1>"),   # tiles16 = 297, partial tiles
+]
+
+
+@pytest.mark.parametrize("shape", POOL_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
+@pytest.mark.parametrize("with_code", [True, False])
+def test_conv3_bench_tiles_pool_bwd(shape, with_code):
+    L, R = _lib(), _rt()
+    N, H, W, cin, cout, want = shape
+    dt = torch.bfloat16
+    torch.manual_seed(14)
+    dy = _rand(N, H, W, cout, dt=dt)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
+    ys = _rand(N, 2 * H, 2 * W, cin, dt=dt)
+    ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
+    psrc = _act_src(ys, ab, kind=L.SRC_POOL_ACT)
+    kw = {}
+    if with_code:
+        pooled = torch.empty(N, H, W, cin, dtype=dt, device="cuda")
+        code = torch.empty(N, H, W, cin, dtype=torch.uint8, device="cuda")
+        L.call("unet_materialize_pool", L.BF16, psrc, N, H, W, pooled.data_ptr(), code.data_ptr(), R.stream())
+        kw["pool_code"] = code.data_ptr()
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    da = torch.zeros(N, 2 * H, 2 * W, cin, device="cuda")
+    d = _conv("bf16", [src], N, H, W, cout, w, 3, L.OUT_POOL_BWD, transpose=True, out=da.data_ptr(),
+              pool_src=_act_src(ys, ab), **kw)
+    assert _variant(d) == want, _variant(d)
+    a = _act_ref(ys, ab).permute(0, 3, 1, 2).requires_grad_(True)
+    F.max_pool2d(a, 2).backward(ref.permute(0, 3, 1, 2))
+    _close_bf16(da.permute(0, 3, 1, 2), a.grad, "pool bwd")
+
+
+@pytest.mark.parametrize("shape", [(4, 512, 512, 64, 64), (4, 256, 256, 64, 128), (4, 64, 64, 512, 512)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_wgrad_bench_sizes(shape):
+    """3x3 weight gradients at the benchmark's sizes (wgrad2, split-K slabs + fixed-order reduction)."""
+    L, R = _lib(), _rt()
+    N, H, W, cin, cout = shape
+    dt = torch.bfloat16
+    torch.manual_seed(15)
+    dy = _rand(N, H, W, cout, dt=dt)
+    ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
+    y = _rand(N, H, W, cin, dt=dt)
+    x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), dy.float().permute(0, 3, 1, 2), padding=1)
+    wd = L.WgradDesc()
+    wd.dtype = R.BF16.code
+    wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = N, H, W, cin, cout, 3, 1
+    wd.src[0] = _act_src(y, ab)
+    wd.dy = dy.data_ptr()
+    dw = torch.empty(cout, cin, 3, 3, device="cuda")
+    wd.dw = dw.data_ptr()
+    ws = torch.empty(max(L.load().unet_wgrad_workspace(wd), 16), dtype=torch.uint8, device="cuda")
+    wd.workspace = ws.data_ptr()
+    L.call("unet_conv_wgrad", wd, R.stream())
+    torch.cuda.synchronize()
+    rel = float((dw - ref).double().norm() / ref.double().norm())
+    assert rel <= 1e-4, rel     # fp32 accumulation of exact bf16 products: only the summation order differs

@@ -55,6 +55,7 @@ class KernelProbe:
     def __init__(self):
         self.target = None
         self.records = []   # (start_event, end_event, algorithmic_flops)
+        self.log = None     # when a list: every probed launch appends (kernel name, output mode)
 
     def enable(self, target: str):
         self.target = target
@@ -66,7 +67,9 @@ class KernelProbe:
     def reset(self):
         self.records = []
 
-    def launch(self, name_fn, flops: float, fn):
+    def launch(self, name_fn, flops: float, fn, mode: Optional[int] = None):
+        if self.log is not None:
+            self.log.append((name_fn(), mode))
         if self.target is None or not name_fn().startswith(self.target):
             return fn()
         s = torch.cuda.Event(enable_timing=True)

@@ -84,7 +84,7 @@ class ConvBN:
             stats = f32(2, self.cout, mt, device=dev)   # [2][C][rows] (unet_conv_stats_rows)
             d.stats = stats.data_ptr()
         probe.launch(lambda: conv_kernel_name(d), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
-                     lambda: L.call("unet_conv", d, stream()))
+                     lambda: L.call("unet_conv", d, stream()), d.out_mode)
         mean = invstd = None
         if use_batch:
             mean = f32(self.cout, device=dev)
@@ -169,7 +169,7 @@ class ConvBN:
             d.out2 = o2.data_ptr() if o2 is not None else None
             d.accum2 = int(dgrad.get("accum2", 0))
         probe.launch(lambda: conv_kernel_name(d), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
-                     lambda: L.call("unet_conv", d, stream()))
+                     lambda: L.call("unet_conv", d, stream()), d.out_mode)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -336,7 +336,7 @@ class ConvTStage:
         self.bias = b.detach().float().contiguous() if b is not None else None
         d.bias = vp(self.bias)
         probe.launch(lambda: conv_kernel_name(d), 2.0 * N * h * w * self.cin * 4 * self.ct,
-                     lambda: L.call("unet_conv", d, stream()))
+                     lambda: L.call("unet_conv", d, stream()), d.out_mode)
         return Act(y, None, False)
 
     def backward(self, prec, d_up: torch.Tensor, pad_t: int, pad_l: int, grads: Grads, need_dx: bool = True):
@@ -379,7 +379,7 @@ class ConvTStage:
         d.accum = acc
         d.split = self.cin
         probe.launch(lambda: conv_kernel_name(d), 2.0 * P * self.cin * 4 * ct,
-                     lambda: L.call("unet_conv", d, stream()))
+                     lambda: L.call("unet_conv", d, stream()), d.out_mode)
 
 
 class UpStage:
