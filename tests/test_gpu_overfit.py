@@ -1,106 +1,85 @@
-"""Overfit parity (SURVEY §8(d) gate; BASELINE north_star "Tumor-Dice on the overfit_test set matching
-reference ±1e-3"): the loop of scripts/overfit_test.py:126-205 — AttentionUNet with deep supervision,
-DeepSupervisionLoss(DiceBCELoss, [1, .4, .2, .1]), Adam, one step per epoch on a fixed batch, then an
-eval-mode (running-statistics) forward and the Tumor Dice 2|P∩G|/(|P|+|G|) — run through the HIP path
-(fp32 operand mode) and through the CPU oracle from the same seeded initial weights and data.
-The optimizer is SGD with momentum rather than the script's Adam: Adam's first steps move every
-parameter by ±lr whatever the gradient's size, so parameters whose gradient is rounding noise (ReLU-dead
-or saturated channels) take opposite full-size steps in two correct implementations, and the
-trajectories part after one step (measured: 3e-4 relative loss difference after step 1).  With SGD the
-update is proportional to the gradient, so the comparison measures the implementation, not Adam's
-sign amplification; an Adam run is checked separately for finiteness and learning.
-The real tumour set is not available offline: the batch is synthetic (discs of 300-1300 px carrying a
-brightness signal, as overfit_test selects slices with > 100 tumour pixels)."""
+"""Overfit parity at BASELINE C1 as the reference runs it (scripts/overfit_test.py:126-205; north_star
+"Tumor-Dice on the overfit_test set matching reference +-1e-3"): AttentionUNet(1, 2,
+deep_supervision=True), base 64, a fixed batch of 2 x 1 x 512^2, Adam(lr=1e-3),
+DeepSupervisionLoss(DiceBCELoss, [1, .4, .2, .1]); each epoch one optimizer step, then an eval-mode
+(running-statistics) forward and Tumor Dice 2|P n G| / (|P| + |G|) on the argmax (:182-205).
 
-import math
+Three executions start from the same seeded weights and batch:
+  * the HIP path (fp32 operand mode);
+  * the reference's network as ATen ops in fp32 on the same GPU (the oracle's restatement; the
+    reference script itself runs on `cuda` when one is present, overfit_test.py:88);
+  * the same in fp64 (the exact-arithmetic yardstick).
+Measured (tools/overfit_diag.py, profiles/r02_overfit_c1.txt): Adam makes the loop sensitive to
+rounding — parameters whose gradient is rounding noise take +-lr steps — so the reference's own fp32 and
+fp64 executions part after a few epochs; over 60 epochs their Tumor-Dice differs by up to 0.5.  The
++-1e-3 target is therefore below the reference's own noise floor.  The stated bound: over the first 16
+epochs (Dice rises from 0.01 to ~0.97), at every epoch our Tumor-Dice is within max(1e-3, 1.5 x S) of
+the fp32 reference, where S is the largest fp32-vs-fp64 Tumor-Dice spread of the reference itself in that
+window; the losses obey the same rule; all three overfit the batch (Dice > 0.8, the script's pass
+criterion, overfit_test.py:288).  The real tumour set is not available offline: the batch is synthetic
+(two discs of ~300-1300 px per image carrying a brightness signal, as overfit_test selects slices with
+> 100 tumour pixels)."""
+
+import sys
+from pathlib import Path
 
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
-
-def _batch(n=2, h=128, w=128, seed=5):
-    g = torch.Generator().manual_seed(seed)
-    t = torch.zeros(n, h, w, dtype=torch.int64)
-    yy, xx = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
-    for i in range(n):
-        for _ in range(2):
-            cy, cx = int(torch.randint(24, h - 24, (1,), generator=g)), int(torch.randint(24, w - 24, (1,), generator=g))
-            r = int(torch.randint(10, 20, (1,), generator=g))
-            t[i][(yy - cy) ** 2 + (xx - cx) ** 2 <= r * r] = 1
-    x = (torch.rand(n, 1, h, w, generator=g) * 2 - 1) * 0.5 + 0.8 * t[:, None].float()
-    return x, t
+EPOCHS = 16
 
 
-def test_overfit_tumor_dice_matches_oracle():
-    from oracle import unet_oracle as O
+def _tools():
+    root = Path(__file__).resolve().parent.parent
+    if str(root / "tools") not in sys.path:
+        sys.path.insert(0, str(root / "tools"))
+    import overfit_diag
+    return overfit_diag
+
+
+def test_overfit_c1_tumor_dice_vs_reference_spread():
+    D = _tools()
     from unet.models import AttentionUNet
-    from unet.utils.loss import DeepSupervisionLoss, DiceBCELoss
-
+    torch.backends.cudnn.deterministic = True
     torch.manual_seed(0)
-    m = AttentionUNet(1, 2, deep_supervision=True, base_features=8)
-    p = O.params_from_module(m)
+    m = AttentionUNet(1, 2, deep_supervision=True, base_features=64)
+    init = {k: v.clone() for k, v in m.state_dict().items()}
     names = [k for k, _ in m.named_parameters()]
-    m = m.cuda().train()
-    m.hip_precision = "fp32"
-    x, t = _batch()
-    xg, tg = x.cuda(), t.cuda()
-    lr, epochs = 0.02, 15
-    opt_h = torch.optim.SGD(m.parameters(), lr=lr, momentum=0.9)
-    opt_o = torch.optim.SGD([p[k] for k in names], lr=lr, momentum=0.9)
-    crit = DeepSupervisionLoss(DiceBCELoss(), weights=[1.0, 0.4, 0.2, 0.1])
-    hist = []
-    for _ in range(epochs):
-        opt_h.zero_grad()
-        loss_h = crit(m(xg), tg)
-        loss_h.backward()
-        opt_h.step()
-        opt_o.zero_grad()
-        out_o = O.attention_unet_forward(p, x, training=True, deep_supervision=True)
-        loss_o = O.deep_supervision_loss(out_o, t, O.dice_bce_loss)
-        loss_o.backward()
-        opt_o.step()
-        m.eval()
-        with torch.no_grad():
-            dice_h = O.tumor_dice(m(xg).argmax(1).cpu(), t)
-            dice_o = O.tumor_dice(O.attention_unet_forward(p, x, training=False).argmax(1), t)
-        m.train()
-        hist.append((float(loss_h.detach()), float(loss_o.detach()), dice_h, dice_o))
-    print("epoch loss_hip loss_oracle dice_hip dice_oracle")
-    for i, h in enumerate(hist):
-        print(i, *h)
-    # early steps: the implementations agree to ~1e-5 (rounding); training then amplifies rounding
-    # differences (batch-statistics BN on a 2-image batch, momentum), so later epochs get a looser bound
-    for i, (lh, lo, dh, do) in enumerate(hist):
-        assert math.isfinite(lh)
-        assert abs(lh - lo) <= (1e-3 if i < 6 else 1e-2) * abs(lo), (i, hist)
-    assert hist[-1][2] > 0.8 and hist[-1][3] > 0.8, hist      # both overfit the tumours
-    assert abs(hist[-1][2] - hist[-1][3]) <= 2e-2, hist
+    x, t = D.batch(2, 512, 512)
+    hip = D.run_hip(init, x, t, EPOCHS, 64)
+    r32 = D.run_oracle(init, names, x, t, EPOCHS, torch.float32)
+    r64 = D.run_oracle(init, names, x, t, EPOCHS, torch.float64)
+    print("\nepoch loss_hip loss_ref32 loss_ref64 | dice_hip dice_ref32 dice_ref64")
+    for i in range(EPOCHS):
+        print(i, *("%.6f" % v for v in (hip[i][0], r32[i][0], r64[i][0], hip[i][1], r32[i][1], r64[i][1])))
+    s_dice = max(abs(a[1] - b[1]) for a, b in zip(r32, r64))
+    s_loss = max(abs(a[0] - b[0]) / abs(b[0]) for a, b in zip(r32, r64))
+    d_dice = max(abs(a[1] - b[1]) for a, b in zip(hip, r32))
+    d_loss = max(abs(a[0] - b[0]) / abs(b[0]) for a, b in zip(hip, r32))
+    print(f"reference fp32-vs-fp64 spread: dice {s_dice:.2e}, loss rel {s_loss:.2e}; "
+          f"HIP-vs-reference fp32: dice {d_dice:.2e}, loss rel {d_loss:.2e}")
+    assert abs(hip[0][0] - r32[0][0]) <= 1e-5 * abs(r32[0][0])       # first step: same weights, fp32 noise
+    assert d_dice <= max(1e-3, 1.5 * s_dice), (d_dice, s_dice)
+    assert d_loss <= max(1e-4, 1.5 * s_loss), (d_loss, s_loss)
+    assert hip[-1][1] > 0.8 and r32[-1][1] > 0.8 and r64[-1][1] > 0.8
 
 
-def test_overfit_adam_learns():
-    """The script's own optimizer (Adam, overfit_test.py:155): the HIP path overfits the batch."""
-    from oracle import unet_oracle as O
+@pytest.mark.skipif(__import__("os").environ.get("UNET_SLOW") != "1", reason="200-epoch run (~3 min); UNET_SLOW=1")
+def test_overfit_c1_full_protocol_final_dice():
+    """The reference's whole protocol (200 epochs, overfit_test.py:69): once converged the trajectories
+    meet again and the final Tumor-Dice agrees within 1e-3 (measured: HIP 0.999018, reference fp32
+    0.999214, fp64 0.998231; profiles/r02_overfit_c1_200ep.txt)."""
+    D = _tools()
     from unet.models import AttentionUNet
-    from unet.utils.loss import DeepSupervisionLoss, DiceBCELoss
-
+    torch.backends.cudnn.deterministic = True
     torch.manual_seed(0)
-    m = AttentionUNet(1, 2, deep_supervision=True, base_features=8).cuda().train()
-    x, t = _batch()
-    xg, tg = x.cuda(), t.cuda()
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
-    crit = DeepSupervisionLoss(DiceBCELoss(), weights=[1.0, 0.4, 0.2, 0.1])
-    losses = []
-    for _ in range(40):
-        opt.zero_grad()
-        loss = crit(m(xg), tg)
-        loss.backward()
-        opt.step()
-        losses.append(float(loss.detach()))
-    m.eval()
-    with torch.no_grad():
-        dice = O.tumor_dice(m(xg).argmax(1).cpu(), t)
-    assert all(math.isfinite(v) for v in losses)
-    assert losses[-1] < 0.7 * losses[0], losses
-    assert dice > 0.5, (dice, losses)
+    m = AttentionUNet(1, 2, deep_supervision=True, base_features=64)
+    init = {k: v.clone() for k, v in m.state_dict().items()}
+    names = [k for k, _ in m.named_parameters()]
+    x, t = D.batch(2, 512, 512)
+    hip = D.run_hip(init, x, t, 200, 64)
+    r32 = D.run_oracle(init, names, x, t, 200, torch.float32)
+    assert abs(hip[-1][1] - r32[-1][1]) <= 1e-3, (hip[-1], r32[-1])
+    assert hip[-1][1] > 0.8
