@@ -99,9 +99,7 @@ def main():
     ap.add_argument("--accum", type=int, default=1, help="micro-batches per optimizer step (C5: 8; scripts/train.py:133-143)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--probe", default=None, help="kernel family to time live (default: conv_kernel<prec,3,64>)")
-    ap.add_argument("--dp", default="overlap", choices=["overlap", "torch-ddp"],
-                    help="N>1 gradient averaging: per-stage overlapped buckets (default) or torch DDP")
-    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--bucket-mb", type=float, default=25.0, help="DDP bucket_cap_mb (N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--cpu-batch", type=int, default=1)
@@ -131,13 +129,12 @@ def main():
     model = (AttentionUNet(args.in_ch, 2) if args.model == "attention_unet" else UNet(args.in_ch, 2)).to(dev).train()
     model.hip_precision = args.precision
     net = model
-    if world > 1 and args.dp == "torch-ddp":
-        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False,
-                                                        gradient_as_bucket_view=True, bucket_cap_mb=100)
-    elif world > 1:
-        # per-stage buckets all-reduced while the remaining stages' backward runs (unet.utils.distributed)
-        from unet.utils.distributed import OverlappedGradSync
-        net = OverlappedGradSync(model, bucket_cap_mb=args.bucket_mb)
+    if world > 1:
+        # stock torch DDP over RCCL: the HIP backward is one autograd node per reference module, so the
+        # reducer all-reduces each full bucket while the remaining stages run (unet.utils.distributed)
+        from unet.utils.distributed import wrap_ddp
+        net = wrap_ddp(model, local if backend == "nccl" else None, bucket_cap_mb=args.bucket_mb,
+                       broadcast_buffers=False)
     opt = torch.optim.AdamW(model.parameters(), lr=5e-5, weight_decay=1e-4, fused=True)
     crit = DiceBCELoss()
     gen = torch.Generator().manual_seed(1234 + rank)
@@ -222,7 +219,7 @@ def main():
                    "model": args.model, "global_batch": world * args.batch * args.accum, "per_gpu_batch": args.batch,
                    "grad_accum": args.accum, "image": [args.in_ch, args.size, args.size],
                    "parallelism": f"dp{world}" if world > 1 else "single",
-                   "grad_sync": args.dp if world > 1 else None},
+                   "grad_sync": f"torch DDP ({backend}, bucket {args.bucket_mb:g} MB)" if world > 1 else None},
         "whole_step_tflops": (round(value * FLOPS_PER_IMAGE[args.model] / 1e12, 2)
                               if (args.size, args.in_ch) == (512, 1) else None),
         "roofline": {"kernel": target, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,

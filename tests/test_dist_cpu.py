@@ -117,70 +117,3 @@ def test_bench_time_is_max_over_ranks():
 def test_single_process_time_passthrough():
     import bench
     assert bench.max_over_ranks(3.5, torch.device("cpu")) == 3.5
-
-
-# ---- OverlappedGradSync (unet.utils.distributed): per-stage buckets, DDP-average semantics ----
-_STAGES = ("outc", "up4", "up3", "up2", "up1", "down4", "down3", "down2", "down1", "inc")
-
-
-def _sync_worker(rank: int, world: int, port: int, q):
-    import sys
-    from pathlib import Path
-    root = Path(__file__).resolve().parent.parent
-    sys.path[:0] = [str(root / "unet-segment-pytorch_amd"), str(root)]
-    _setup(rank, world, port)
-    from unet.models import AttentionUNet
-    from unet.utils.distributed import OverlappedGradSync
-    torch.manual_seed(rank)                      # different init per rank: the sync must broadcast rank 0's
-    m = AttentionUNet(1, 2, base_features=4)
-    sync = OverlappedGradSync(m, bucket_cap_mb=0.002)   # tiny cap: several buckets
-    named = dict(m.named_parameters())
-
-    def backward(g_by_name):
-        # NetworkPlan.backward order: a stage's gradients appear, then the hook runs
-        grads = {}
-        for st in _STAGES:
-            for k, v in g_by_name.items():
-                if k.split(".")[0] == st:
-                    grads[named[k]] = v.clone()
-            sync.stage_done(grads)
-        n_buckets = len(sync._buckets)
-        sync.finish(grads)
-        return {k: grads[p] for k, p in named.items() if p in grads}, n_buckets
-
-    g = _grads(rank)
-    avg, nb = backward(g)
-    # accumulation: micro-batch A under no_sync (autograd leaves it in p.grad), micro-batch B synchronised
-    ga = _grads(rank + 2)
-    with sync.no_sync():
-        backward(ga)                             # no exchange, returns local grads untouched
-    for k, p in named.items():
-        p.grad = ga[k].clone()
-    acc, _ = backward(g)
-    cleared = all(p.grad is None for p in named.values())
-    w0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
-    if rank == 0:
-        q.put(({k: v.numpy() for k, v in avg.items()}, {k: v.numpy() for k, v in acc.items()}, nb, cleared,
-               {k: v.numpy() for k, v in w0.items()}))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_overlapped_grad_sync_matches_ddp_average():
-    (res,) = _run(_sync_worker, 2)
-    avg, acc, n_buckets, cleared, w0 = res
-    assert n_buckets >= 3 and cleared
-    torch.manual_seed(0)
-    from unet.models import AttentionUNet
-    ref_w = AttentionUNet(1, 2, base_features=4).state_dict()
-    for k, v in w0.items():                      # rank 0's init broadcast
-        if k.endswith("weight") or k.endswith("bias"):
-            assert torch.equal(torch.from_numpy(v), ref_w[k]), k
-    g0, g1, a0, a1 = _grads(0), _grads(1), _grads(2), _grads(3)
-    assert set(avg) == set(g0)
-    worst = 0.0
-    for k in g0:   # relative to the tensor's max: fp32 reduction-order noise (workers run single-threaded)
-        for got, want in ((avg[k], (g0[k] + g1[k]) / 2), (acc[k], (g0[k] + a0[k] + g1[k] + a1[k]) / 2)):
-            d = (torch.from_numpy(got) - want).abs().max().item()
-            worst = max(worst, d / (want.abs().max().item() + 1e-12))
-    assert worst < 1e-4, worst

@@ -1,6 +1,7 @@
 """autograd.Function wrappers: the reference's modules as HIP launch plans.
 
-`run_network` serves UNet / AttentionUNet (whole-network plan with cross-module fusion);
+`run_network` serves UNet / AttentionUNet (whole-network plan with cross-module fusion, one autograd
+node per reference module so DDP's reducer sees each stage's parameter gradients as soon as they exist);
 `run_module` serves a standalone DoubleConv / Down / Up / AttentionUp / AttentionGate / OutConv call
 (NCHW fp32 in and out, exactly like the reference module).  Param grads are returned through
 autograd, so `loss.backward()`, DDP hooks, clip_grad_norm_ and optimizers work unchanged.
@@ -48,6 +49,39 @@ def _apply(plan, module: torch.nn.Module, inputs: List[torch.Tensor]):
 
 
 # ------------------------------------------------------------------------------------------------
+class _Stage:
+    """One autograd node of the network plan: `fwd()` runs the stage's launches and returns its
+    output (a real tensor, or an empty token standing for the stage's virtual activation); `bwd(gouts,
+    grads)` runs its backward launches and returns the gradients of its tensor inputs."""
+
+    __slots__ = ("fwd", "bwd", "params")
+
+    def __init__(self, fwd, bwd, params):
+        self.fwd, self.bwd, self.params = fwd, bwd, params
+
+
+class _StageFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, st: _Stage, n_in: int, *tensors):
+        ctx.set_materialize_grads(False)     # unused outputs (a DS head outside the loss) stay None
+        ctx.st, ctx.n_in = st, n_in
+        return st.fwd()
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, *gouts):
+        st = ctx.st
+        grads = Grads()
+        dins = st.bwd(list(gouts), grads)
+        ctx.st = None
+        return (None, None, *dins, *[grads.get(p) for p in st.params])
+
+
+def _stage(fwd, bwd, module, inputs: List[torch.Tensor]):
+    params = [p for p in module.parameters()] if module is not None else []
+    return _StageFn.apply(_Stage(fwd, bwd, params), len(inputs), *inputs, *params)
+
+
 class _NetPlan:
     def __init__(self, model, attention: bool):
         self.model = model
@@ -55,22 +89,55 @@ class _NetPlan:
         self.training = model.training
         self.net = NetworkPlan(model, attention)
 
-    def forward(self, inputs, needs):
-        x = inputs[0]
-        if x.dtype != torch.float32 or not x.is_contiguous():
-            x = x.float().contiguous()
-        return self.net.forward(self.prec, x, self.training, needs[0])
+    def run(self, x: torch.Tensor, track: bool):
+        """Untracked: one pass over the plan.  Tracked: one autograd node per reference module, linked by
+        tokens along the data flow (x -> inc -> down1..4, skips into up1..4 -> outc / DS heads)."""
+        net, m = self.net, self.model
+        if not track:
+            return net.forward(self.prec, x, self.training, False)
+        net.begin(self.prec, x, self.training, x.requires_grad)
+        dev = x.device
 
-    def backward(self, gouts, grads):
-        return [self.net.backward(self.prec, gouts, grads)]
+        def token():
+            return torch.empty(0, device=dev)
+
+        def fwd_tok(f, *a):
+            def run():
+                f(*a)
+                return token()
+            return run
+
+        def bwd_none(f, n_in, *a):
+            def run(gouts, grads):
+                f(*a, grads)
+                return [None] * n_in
+            return run
+
+        t = [_stage(fwd_tok(net.fwd_inc), lambda g, grads: [net.bwd_inc(grads)], m.inc, [x])]
+        for i in range(4):
+            t.append(_stage(fwd_tok(net.fwd_down, i), bwd_none(net.bwd_down, 1, i), getattr(m, f"down{i + 1}"),
+                            [t[-1]]))
+        dec = []
+        y = t[4]
+        for i in range(4):
+            y = _stage(fwd_tok(net.fwd_up, i), bwd_none(net.bwd_up, 2, i), getattr(m, f"up{i + 1}"), [y, t[3 - i]])
+            dec.append(y)
+        outs = [_stage(net.fwd_outc, lambda g, grads: (net.bwd_outc(g[0], grads), [None])[1], m.outc, [dec[3]])]
+        if net.with_ds:
+            for k, (mod, src) in enumerate(((m.ds_out1, dec[2]), (m.ds_out2, dec[1]), (m.ds_out3, dec[0]))):
+                outs.append(_stage(lambda k=k: net.fwd_head(k),
+                                   lambda g, grads, k=k: (net.bwd_head(k, g[0], grads), [None])[1], mod, [src]))
+        return outs
 
 
 def run_network(model, x: torch.Tensor, attention: bool):
     require_device(x)
     if x.dim() != 4 or x.shape[1] != model.n_channels:
         raise RuntimeError(f"expected input of shape (N, {model.n_channels}, H, W), got {tuple(x.shape)}")
-    outs = _apply(_NetPlan(model, attention), model, [x])
-    return outs
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.float().contiguous()
+    track = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in model.parameters()))
+    return _NetPlan(model, attention).run(x, track)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -538,7 +538,16 @@ class DSHeadStage:
 
 # ------------------------------------------------------------------------------------------------
 class NetworkPlan:
-    """UNet.forward (unet.py:67-92) / AttentionUNet.forward (unet.py:175-211) as one launch plan."""
+    """UNet.forward (unet.py:67-92) / AttentionUNet.forward (unet.py:175-211) as a launch plan.
+
+    The plan is cut at the reference's module boundaries: inc, down1..4, up1..4, outc and the deep-
+    supervision heads each have a forward piece (`fwd_*`) and a backward piece (`bwd_*`).  Under
+    autograd every piece is its own node (`_hip.functions`), linked by empty "token" tensors along the
+    reference's data flow (skip connections included), so a stage's parameter gradients are handed to
+    autograd — and to DistributedDataParallel's reducer hooks — as soon as that stage's backward is done.
+    Activation gradients do not travel through autograd: consumers accumulate them into the producer's
+    `Act.grad` buffer, and the token graph guarantees that a producer runs its backward only after every
+    consumer has."""
 
     def __init__(self, model, attention: bool):
         self.model = model
@@ -562,68 +571,89 @@ class NetworkPlan:
                 out += [u.gate.cg, u.gate.cx]
         return out
 
-    def forward(self, prec: Precision, x: torch.Tensor, training: bool, need_dx: bool):
-        N, C, H, W = x.shape
-        self.x = x
-        self.need_dx = need_dx
+    # ---- forward pieces ----
+    def begin(self, prec: Precision, x: torch.Tensor, training: bool, need_dx: bool):
+        self.prec, self.training, self.x, self.need_dx = prec, training, x, need_dx
+        self.with_ds = self.ds and training
+        self._bwd_packed = False
         cbs = self.convbns()
         for cb, wp in zip(cbs, pack_many([(cb.conv.weight, False) for cb in cbs], prec)):
             cb.pre_wp = wp
-        xs = [self.inc.forward(prec, [_nchw(x)], N, H, W, training, keep=x)]
-        for d in self.downs:
-            xs.append(d.forward(prec, xs[-1], training))
-        self.xs = xs
-        y = xs[4]
-        dec = []
-        for i, u in enumerate(self.ups):
-            y = u.forward(prec, y, xs[3 - i], training)
-            dec.append(y)
-        self.dec = dec     # d4, d3, d2, d1
-        logits = self.outc.forward(prec, y)
-        self.with_ds = self.ds and training
-        if self.with_ds:
-            # [logits, ds1(d2), ds2(d3), ds3(d4)]
-            outs = [logits]
-            for head, a in zip(self.heads, (dec[2], dec[1], dec[0])):
-                outs.append(head.forward(prec, a, H, W))
-            return outs
-        return [logits]
+        self.xs, self.dec = [], []
 
-    def backward(self, prec: Precision, gouts, grads: Grads):
-        cbs = [cb for cb in self.convbns() if cb is not self.inc.c1 or self.need_dx]
-        for cb, wt in zip(cbs, pack_many([(cb.conv.weight, True) for cb in cbs], prec)):
-            cb.pre_wt = wt
-        gl = gouts[0]
-        if gl is None:
-            gl = torch.zeros(self.x.shape[0], self.outc.k, self.x.shape[2], self.x.shape[3], device=self.x.device)
-        # data-parallel gradient averaging overlapped with the remaining stages (unet.utils.distributed)
-        sync = getattr(self.model, "_grad_sync", None)
-        hook = sync.stage_done if sync is not None else (lambda g: None)
-        self.outc.backward(prec, gl, grads)
+    def fwd_inc(self):
+        N, C, H, W = self.x.shape
+        self.xs = [self.inc.forward(self.prec, [_nchw(self.x)], N, H, W, self.training, keep=self.x)]
+
+    def fwd_down(self, i: int):
+        self.xs.append(self.downs[i].forward(self.prec, self.xs[-1], self.training))
+
+    def fwd_up(self, i: int):
+        y = self.xs[4] if i == 0 else self.dec[-1]
+        self.dec.append(self.ups[i].forward(self.prec, y, self.xs[3 - i], self.training))   # d4, d3, d2, d1
+
+    def fwd_outc(self) -> torch.Tensor:
+        return self.outc.forward(self.prec, self.dec[-1])
+
+    def fwd_head(self, k: int) -> torch.Tensor:
+        """[ds1(d2), ds2(d3), ds3(d4)][k] resized to the input size (unet.py:204-209)."""
+        return self.heads[k].forward(self.prec, (self.dec[2], self.dec[1], self.dec[0])[k], self.x.shape[2],
+                                     self.x.shape[3])
+
+    def forward(self, prec: Precision, x: torch.Tensor, training: bool, need_dx: bool):
+        """The whole forward in one go (no autograd: eval / no_grad)."""
+        self.begin(prec, x, training, need_dx)
+        self.fwd_inc()
+        for i in range(4):
+            self.fwd_down(i)
+        for i in range(4):
+            self.fwd_up(i)
+        outs = [self.fwd_outc()]
         if self.with_ds:
-            for head, g in zip(self.heads, gouts[1:]):
-                if g is not None:
-                    head.backward(prec, g, grads)
-        hook(grads)
-        for u in reversed(self.ups):
-            u.backward(prec, grads)
-            hook(grads)
-        for d in reversed(self.downs):
-            d.backward(prec, grads)
-            hook(grads)
-        dx = None
-        if self.need_dx:
+            outs += [self.fwd_head(k) for k in range(3)]     # [logits, ds1(d2), ds2(d3), ds3(d4)]
+        return outs
+
+    # ---- backward pieces (run by autograd in reverse data-flow order) ----
+    def prepare_backward(self):
+        """Pack every transposed (dgrad) weight in one launch, once per backward pass."""
+        if self._bwd_packed:
+            return
+        self._bwd_packed = True
+        cbs = [cb for cb in self.convbns() if cb is not self.inc.c1 or self.need_dx]
+        for cb, wt in zip(cbs, pack_many([(cb.conv.weight, True) for cb in cbs], self.prec)):
+            cb.pre_wt = wt
+
+    def bwd_outc(self, g: Optional[torch.Tensor], grads: Grads):
+        self.prepare_backward()
+        if g is None:
             x = self.x
-            N, C, H, W = x.shape
-            gx = f32(N, H, W, C, device=x.device)
-            self.inc.backward(prec, grads, {"mode": "f32", "out": gx, "accum": 0})
-            from .runtime import grad_nhwc_to_nchw
-            dx = grad_nhwc_to_nchw(gx)
-        else:
-            self.inc.backward(prec, grads, None)
-        if sync is not None:
-            sync.finish(grads)
-        return dx
+            g = torch.zeros(x.shape[0], self.outc.k, x.shape[2], x.shape[3], device=x.device)
+        self.outc.backward(self.prec, g, grads)
+
+    def bwd_head(self, k: int, g: Optional[torch.Tensor], grads: Grads):
+        self.prepare_backward()
+        if g is not None:
+            self.heads[k].backward(self.prec, g, grads)
+
+    def bwd_up(self, i: int, grads: Grads):
+        self.prepare_backward()
+        self.ups[i].backward(self.prec, grads)
+
+    def bwd_down(self, i: int, grads: Grads):
+        self.prepare_backward()
+        self.downs[i].backward(self.prec, grads)
+
+    def bwd_inc(self, grads: Grads) -> Optional[torch.Tensor]:
+        self.prepare_backward()
+        if not self.need_dx:
+            self.inc.backward(self.prec, grads, None)
+            return None
+        x = self.x
+        N, C, H, W = x.shape
+        gx = f32(N, H, W, C, device=x.device)
+        self.inc.backward(self.prec, grads, {"mode": "f32", "out": gx, "accum": 0})
+        from .runtime import grad_nhwc_to_nchw
+        return grad_nhwc_to_nchw(gx)
 
 
 def _nchw(x: torch.Tensor) -> L.Src:

@@ -1,122 +1,32 @@
-"""Data-parallel gradient averaging overlapped with the HIP backward.
+"""Data-parallel training over RCCL.
 
-The reference trains data-parallel by batch (scripts/train.py:133-143 gradient accumulation; the
-multi-GPU row of BASELINE.json wraps the model in DDP).  Under torch DDP our whole-network backward is
-ONE autograd node, so every gradient becomes ready at the same instant and the ~70 MB all-reduce runs
-after the last weight gradient, fully exposed.  `OverlappedGradSync` instead receives a callback from
-`NetworkPlan.backward` after every stage (outc, up4 .. up1, down4 .. down1, inc): the gradients that
-stage just produced are packed into a flat bucket and averaged with an async all-reduce (RCCL on ROCm,
-running on its own stream) while the next stage's dgrad/wgrad kernels keep the CUs busy.  The deep
-stages, which hold most of the parameters, finish first, so only the small `inc` bucket is exposed.
+The reference trains on one device and reaches its effective batch by gradient accumulation
+(scripts/train.py:133-143); this path shards the batch over the GPUs of a node instead, one process
+per GPU, with PyTorch's own `DistributedDataParallel` (backend "nccl" = RCCL on ROCm, over xGMI).
+Nothing here re-implements DDP: the network's backward runs as one autograd node per reference module
+(`unet._hip.functions`), so DDP's reducer marks a stage's parameters ready the moment that stage's
+backward has finished and all-reduces full buckets while the remaining stages' kernels run.  The
+backward visits outc, up4 .. up1, down4 .. down1, inc; the deep stages hold most of the 17.6 M
+parameters, so only the last (small) bucket is exposed.
 
-Semantics are DDP's: gradients are averaged over ranks; `no_sync()` skips the exchange for the
-first accum-1 micro-batches and the synchronised micro-batch folds the locally accumulated `p.grad`
-into its buckets (so the result equals DDP's).  Only the whole-network path (UNet / AttentionUNet
-forward) calls the hooks; modules used standalone keep working under torch DDP.
+Gradient accumulation keeps the reference's loop: the first accum-1 micro-batches under
+`ddp.no_sync()`, loss / accum on each, one synchronised backward, then clip + optimizer step.
 """
 
 from __future__ import annotations
 
-import contextlib
-from typing import Dict, List, Optional
+from typing import Optional
 
 import torch
-import torch.distributed as dist
+from torch.nn.parallel import DistributedDataParallel
 
 
-class OverlappedGradSync:
-    """Attach to a UNet / AttentionUNet: ``sync = OverlappedGradSync(model, bucket_cap_mb=32)``.
-
-    Broadcasts rank 0's parameters (and buffers when ``broadcast_buffers``) at construction, as DDP
-    does, so every replica starts from the same weights.
-    """
-
-    def __init__(self, model: torch.nn.Module, process_group=None, bucket_cap_mb: float = 32.0,
-                 broadcast_buffers: bool = False):
-        if not dist.is_initialized():
-            raise RuntimeError("OverlappedGradSync needs an initialised torch.distributed process group")
-        self.model = model
-        self.pg = process_group
-        self.world = dist.get_world_size(process_group)
-        self.cap = int(bucket_cap_mb * (1 << 20))
-        self.params = [p for p in model.parameters() if p.requires_grad]
-        self._pid = {id(p): i for i, p in enumerate(self.params)}
-        self.enabled = True
-        self._reset()
-        with torch.no_grad():
-            for p in model.parameters():
-                dist.broadcast(p.data, 0, group=process_group)
-            if broadcast_buffers:
-                for b in model.buffers():
-                    dist.broadcast(b, 0, group=process_group)
-        model._grad_sync = self
-
-    # ---- DDP-compatible surface ----
-    @contextlib.contextmanager
-    def no_sync(self):
-        prev, self.enabled = self.enabled, False
-        try:
-            yield
-        finally:
-            self.enabled = prev
-
-    def __call__(self, *args, **kwargs):
-        return self.model(*args, **kwargs)
-
-    # ---- hooks called by NetworkPlan.backward ----
-    def _reset(self):
-        self._done = set()           # params already packed into a bucket this backward
-        self._pending: List[torch.Tensor] = []
-        self._pending_bytes = 0
-        self._buckets = []           # (flat, [params], work)
-
-    def stage_done(self, grads: Dict[torch.nn.Parameter, torch.Tensor], final: bool = False):
-        """Pack every gradient that is now complete and not yet bucketed; launch full buckets."""
-        if not self.enabled:
-            return
-        for p in grads:
-            if id(p) in self._pid and id(p) not in self._done:
-                self._done.add(id(p))
-                self._pending.append(p)
-                self._pending_bytes += p.numel() * 4
-        if self._pending and (final or self._pending_bytes >= self.cap):
-            self._launch(grads)
-
-    def _launch(self, grads):
-        ps = self._pending
-        self._pending, self._pending_bytes = [], 0
-        flat = torch.cat([grads[p].reshape(-1).float() for p in ps])
-        off = 0
-        for p in ps:
-            n = p.numel()
-            if p.grad is not None:          # locally accumulated micro-batches (no_sync)
-                flat[off:off + n].add_(p.grad.reshape(-1))
-            off += n
-        # divide, then SUM: DDP's own default (and every backend has SUM; gloo has no AVG)
-        flat.div_(self.world)
-        work = dist.all_reduce(flat, group=self.pg, async_op=True)
-        self._buckets.append((flat, ps, work))
-
-    def finish(self, grads: Dict[torch.nn.Parameter, torch.Tensor]):
-        """Wait for every bucket (stream-ordered on NCCL) and hand out views of the averaged buckets.
-
-        Parameters whose local `p.grad` was folded into a bucket get `p.grad = None`, so autograd's
-        accumulation assigns the averaged total instead of adding to it.
-        """
-        if not self.enabled:
-            return
-        self.stage_done(grads, final=True)
-        for flat, ps, work in self._buckets:
-            work.wait()
-            off = 0
-            for p in ps:
-                n = p.numel()
-                grads[p] = flat[off:off + n].view_as(p)
-                if p.grad is not None:
-                    p.grad = None
-                off += n
-        self._reset()
-
-
-def grad_sync_of(model: torch.nn.Module) -> Optional[OverlappedGradSync]:
-    return getattr(model, "_grad_sync", None)
+def wrap_ddp(model: torch.nn.Module, device_id: Optional[int] = None, bucket_cap_mb: float = 25.0,
+             broadcast_buffers: bool = True, **kwargs) -> DistributedDataParallel:
+    """`DistributedDataParallel(model)` with the settings this path is measured with:
+    `gradient_as_bucket_view=True` (no second copy of the 70 MB of gradients) and DDP's defaults
+    otherwise.  `broadcast_buffers=False` keeps each rank's BN running statistics local (one collective
+    less per forward; the reference's running statistics only matter in eval mode)."""
+    return DistributedDataParallel(model, device_ids=[device_id] if device_id is not None else None,
+                                   bucket_cap_mb=bucket_cap_mb, broadcast_buffers=broadcast_buffers,
+                                   gradient_as_bucket_view=True, **kwargs)
