@@ -249,6 +249,19 @@ int unet_loss_finalize(const float* partial, int rows, long long N, int K, float
 int unet_loss_grad(long long N, int K, long long HW, const float* z, const int64_t* t, const float* coef,
                    const float* gout, int gout_per_elem, int ignore_bg, float* dz, void* stream);
 
+/* ---- DeepSupervisionLoss(base) over S <= 4 logit sets — loss.py:194-229 ----------------------
+ * The sets [main, ds1, ds2, ds3] (same shape, shared targets; unet.py:204-209) go through ONE launch
+ * of each pass: partial [S][N][rows][4+3K], coef [S][N][2+2K] (scaled by set_weights[s]),
+ * loss = sum_s set_weights[s] * base_loss_s (host arrays z / dz / set_weights of S entries).       */
+int unet_loss_reduce_multi(int S, long long N, int K, long long HW, const float* const* z, const int64_t* t,
+                           float* partial, void* stream);
+int unet_loss_finalize_multi(const float* partial, int rows, int S, const float* set_weights, long long N, int K,
+                             float ce_w, float dice_w, float class_w, float ce_smooth, float dice_smooth,
+                             int ignore_bg, int reduction, float* loss, float* coef, void* stream);
+int unet_loss_grad_multi(int S, long long N, int K, long long HW, const float* const* z, const int64_t* t,
+                         const float* coef, const float* gout, int gout_per_elem, int ignore_bg, float* const* dz,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -134,3 +134,37 @@ def test_loss_three_classes(golden_losses):
     loss.backward()
     assert abs(float(loss) - float(ref["loss"])) <= 1e-5 * (1 + abs(float(ref["loss"])))
     assert max_abs(z.grad, ref["grad"]) <= 1e-6 + 1e-4 * float(ref["grad"].abs().max())
+
+
+@pytest.mark.parametrize("base", ["dice_bce", "dice", "balanced_ce", "dice_bce_w"])
+@pytest.mark.parametrize("K", [2, 3])
+def test_deep_supervision_fused_vs_oracle(golden_losses, base, K):
+    """DeepSupervisionLoss over [main, ds1, ds2, ds3] (loss.py:194-229) through one reduce / finalize /
+    grad launch (unet_loss_*_multi) vs the oracle's per-set sum, incl. the gradient of every set."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from oracle import unet_oracle as O
+    from unet.utils.loss import BalancedCELoss, DeepSupervisionLoss, DiceBCELoss, DiceLoss
+    t = golden_losses["t"].clone()
+    if K == 3:
+        t[0, :5, :7] = 2
+    g = torch.Generator().manual_seed(7 + K)
+    zs = [torch.randn(t.shape[0], K, t.shape[1], t.shape[2], generator=g) * s for s in (2.0, 1.0, 0.5, 3.0)]
+    crit, ref_base = {
+        "dice_bce": (DiceBCELoss(), O.dice_bce_loss),
+        "dice": (DiceLoss(), O.dice_loss),
+        "balanced_ce": (BalancedCELoss(), O.balanced_ce_loss),
+        "dice_bce_w": (DiceBCELoss(ce_weight=0.7, dice_weight=1.3, class_weight=0.3),
+                       lambda z, t: O.dice_bce_loss(z, t, 0.7, 1.3, 0.3)),
+    }[base]
+    ds = DeepSupervisionLoss(crit)
+    zg = [z.cuda().requires_grad_(True) for z in zs]
+    loss = ds(zg, t.cuda())
+    loss.backward()
+    zr = [z.clone().requires_grad_(True) for z in zs]
+    ref = O.deep_supervision_loss(zr, t, ref_base)
+    ref.backward()
+    assert abs(float(loss.detach()) - float(ref)) <= 1e-5 * (1 + abs(float(ref))), (float(loss), float(ref))
+    for a, b in zip(zg, zr):
+        assert max_abs(a.grad, b.grad) <= 1e-6 + 1e-4 * float(b.grad.abs().max())

@@ -8,11 +8,22 @@
 //   G_c = gA_nc [t=c] + gB_nc,  w_t = BalancedCE per-pixel weight (labels 0/1 only, loss.py:136-145).
 // The per-image Python loop with boolean-mask indexing of the reference (loss.py:134-145) becomes
 // these device reductions: no host synchronisation.
+// Deep supervision (DeepSupervisionLoss, loss.py:194-229; unet.py:204-209): the S = 4 logit sets
+// [main, ds1, ds2, ds3] share the targets, so one launch of each pass covers all of them (blockIdx.z /
+// the grid-stride index select the set) and the finalize forms Σ_s w_s · loss_s and per-set
+// coefficients already scaled by w_s.
 #include "common.h"
 
 namespace unet {
 
 constexpr int LMAXK = 16;
+constexpr int LMAXS = 4;   // logit sets per launch (deep supervision: main + 3 heads)
+
+struct LossSets {
+  const float* z[LMAXS];
+  float* dz[LMAXS];
+  float w[LMAXS];
+};
 
 static inline int loss_rows(long long HW) {
   long long r = (HW + 4095) / 4096;
@@ -22,12 +33,14 @@ static inline int loss_rows(long long HW) {
 }
 
 template <int KT>
-__global__ void loss_reduce_kernel(long long N, int K_, long long HW, const float* z, const int64_t* t, float* part,
+__global__ void loss_reduce_kernel(long long N, int K_, long long HW, const LossSets sets, const int64_t* t, float* part,
                                    int rows) {
   __shared__ float sh[8];
   const int K = KT ? KT : K_;
   const int F = 4 + 3 * K;
   const long long n = blockIdx.y;
+  const float* z = sets.z[blockIdx.z];
+  part += (size_t)blockIdx.z * N * rows * F;
   const long long per = (HW + rows - 1) / rows;
   const long long q0 = blockIdx.x * per, q1 = min(HW, q0 + per);
   float acc[4 + 3 * (KT ? KT : LMAXK)];
@@ -71,12 +84,12 @@ __global__ void loss_reduce_kernel(long long N, int K_, long long HW, const floa
   }
 }
 
-// one block: (1) one wave per (image, field) pair sums the partial rows in fp64 (fixed order per
-// lane, then a fixed shuffle tree); (2) one thread per image forms its terms; (3) thread 0 combines
-// coef layout [N][2 + 2K]: w0, w1, gA[K], gB[K]
-__global__ void loss_finalize_kernel(const float* part, int rows, long long N, int K, float ce_w, float dice_w,
-                                     float class_w, float ce_smooth, float dice_smooth, int ignore_bg, int reduction,
-                                     float* loss, float* coef) {
+// one block: per set s (1) one wave per (image, field) pair sums the partial rows in fp64 (fixed order
+// per lane, then a fixed shuffle tree); (2) one thread per image forms its terms; (3) thread 0 combines.
+// coef layout [S][N][2 + 2K]: w0, w1, gA[K], gB[K] (already scaled by the set weight); loss: Σ_s w_s loss_s
+__global__ void loss_finalize_kernel(const float* part, int rows, int S, const LossSets sets, long long N, int K,
+                                     float ce_w, float dice_w, float class_w, float ce_smooth, float dice_smooth,
+                                     int ignore_bg, int reduction, float* loss, float* coef) {
   extern __shared__ double dsh[];  // [N] ce terms, [N*K] dice terms, [N*F] field sums
   const int F = 4 + 3 * K;
   const int c_lo = (ignore_bg && K > 1) ? 1 : 0;
@@ -84,67 +97,78 @@ __global__ void loss_finalize_kernel(const float* part, int rows, long long N, i
   const double wred = reduction == 0 ? 1.0 / ((double)N * nd) : 1.0;  // mean / sum / none(=1, gout per elem)
   double* fs = dsh + N + N * K;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (long long pf = wave; pf < N * F; pf += nw) {
-    const long long n = pf / F;
-    const int f = (int)(pf % F);
-    double a = 0;
-    for (int r = lane; r < rows; r += 64) a += part[((size_t)n * rows + r) * F + f];
+  double total = 0;
+  for (int si = 0; si < S; ++si) {
+    const float* ps = part + (size_t)si * N * rows * F;
+    const double ws = sets.w[si];
+    for (long long pf = wave; pf < N * F; pf += nw) {
+      const long long n = pf / F;
+      const int f = (int)(pf % F);
+      double a = 0;
+      for (int r = lane; r < rows; r += 64) a += ps[((size_t)n * rows + r) * F + f];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-    if (lane == 0) fs[pf] = a;
-  }
-  __syncthreads();
-  for (long long n = threadIdx.x; n < N; n += blockDim.x) {
-    const double* s = fs + n * F;
-    const double n0 = (double)(float)(s[0]) + ce_smooth, n1 = (double)(float)(s[1]) + ce_smooth;
-    const double w0 = (1.0 - class_w) / n0, w1 = class_w / n1;
-    dsh[n] = w0 * s[2] + w1 * s[3];
-    float* cf = coef + n * (2 + 2 * K);
-    cf[0] = (float)(ce_w * w0 / (double)N);
-    cf[1] = (float)(ce_w * w1 / (double)N);
-    for (int c = 0; c < K; ++c) {
-      const double I = s[4 + 3 * c], P = s[4 + 3 * c + 1], T = s[4 + 3 * c + 2];
-      const double U = P + T + dice_smooth;
-      const double D = (2.0 * I + dice_smooth) / U;
-      double gA = 0, gB = 0;
-      if (c >= c_lo) {
-        gA = -2.0 * dice_w * wred / U;
-        gB = dice_w * wred * (2.0 * I + dice_smooth) / (U * U);
+      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+      if (lane == 0) fs[pf] = a;
+    }
+    __syncthreads();
+    for (long long n = threadIdx.x; n < N; n += blockDim.x) {
+      const double* s = fs + n * F;
+      const double n0 = (double)(float)(s[0]) + ce_smooth, n1 = (double)(float)(s[1]) + ce_smooth;
+      const double w0 = (1.0 - class_w) / n0, w1 = class_w / n1;
+      dsh[n] = w0 * s[2] + w1 * s[3];
+      float* cf = coef + ((size_t)si * N + n) * (2 + 2 * K);
+      cf[0] = (float)(ws * ce_w * w0 / (double)N);
+      cf[1] = (float)(ws * ce_w * w1 / (double)N);
+      for (int c = 0; c < K; ++c) {
+        const double I = s[4 + 3 * c], P = s[4 + 3 * c + 1], T = s[4 + 3 * c + 2];
+        const double U = P + T + dice_smooth;
+        const double D = (2.0 * I + dice_smooth) / U;
+        double gA = 0, gB = 0;
+        if (c >= c_lo) {
+          gA = -2.0 * ws * dice_w * wred / U;
+          gB = ws * dice_w * wred * (2.0 * I + dice_smooth) / (U * U);
+        }
+        cf[2 + c] = (float)gA;
+        cf[2 + K + c] = (float)gB;
+        dsh[N + n * K + c] = D;
       }
-      cf[2 + c] = (float)gA;
-      cf[2 + K + c] = (float)gB;
-      dsh[N + n * K + c] = D;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (reduction == 2) {  // DiceLoss(reduction='none'): per-(n, c) 1 - D (single set)
+        for (long long n = 0; n < N; ++n)
+          for (int c = c_lo; c < K; ++c) loss[n * nd + (c - c_lo)] = (float)(1.0 - dsh[N + n * K + c]);
+      } else {
+        double ce = 0, dsum = 0;
+        for (long long n = 0; n < N; ++n) {
+          ce += dsh[n];
+          for (int c = c_lo; c < K; ++c) dsum += dsh[N + n * K + c];
+        }
+        ce /= (double)N;
+        const double dl = reduction == 0 ? 1.0 - dsum / ((double)N * nd) : (double)N * nd - dsum;
+        total += ws * (ce_w * ce + dice_w * dl);
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (reduction == 2) {  // DiceLoss(reduction='none'): per-(n, c) 1 - D
-      for (long long n = 0; n < N; ++n)
-        for (int c = c_lo; c < K; ++c) loss[n * nd + (c - c_lo)] = (float)(1.0 - dsh[N + n * K + c]);
-      return;
-    }
-    double ce = 0, dsum = 0;
-    for (long long n = 0; n < N; ++n) {
-      ce += dsh[n];
-      for (int c = c_lo; c < K; ++c) dsum += dsh[N + n * K + c];
-    }
-    ce /= (double)N;
-    double dl = reduction == 0 ? 1.0 - dsum / ((double)N * nd) : (double)N * nd - dsum;
-    loss[0] = (float)(ce_w * ce + dice_w * dl);
-  }
+  if (threadIdx.x == 0 && reduction != 2) loss[0] = (float)total;
 }
 
 template <int KT>
-__global__ void loss_grad_kernel(long long N, int K_, long long HW, const float* z, const int64_t* t, const float* coef,
-                                 const float* gout, int gout_per_elem, int c_lo, float* dz) {
+__global__ void loss_grad_kernel(int S, long long N, int K_, long long HW, const LossSets sets, const int64_t* t,
+                                 const float* coef, const float* gout, int gout_per_elem, int c_lo) {
   constexpr int KM = KT ? KT : LMAXK;
   const int K = KT ? KT : K_;
   const long long total = N * HW;
   const int nd = K - c_lo;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const long long n = e / HW, q = e % HW;
-    const float* zp = z + n * K * HW + q;
-    const float* cf = coef + n * (2 + 2 * K);
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total * S;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int si = (int)(e / total);
+    const long long en = e - (long long)si * total;
+    const long long n = en / HW, q = en % HW;
+    const float* zp = sets.z[si] + n * K * HW + q;
+    float* dz = sets.dz[si];
+    const float* cf = coef + ((size_t)si * N + n) * (2 + 2 * K);
     float p[KM];
     float m = -INFINITY;
 #pragma unroll
@@ -188,40 +212,80 @@ extern "C" {
 
 int unet_loss_rows(long long HW) { return loss_rows(HW); }
 
-int unet_loss_reduce(long long N, int K, long long HW, const float* z, const int64_t* t, float* partial, void* stream) {
+static int load_sets(int S, const float* const* z, float* const* dz, const float* w, LossSets& ls) {
+  if (S < 1 || S > LMAXS || !z) { set_error("unet_loss: 1 to 4 logit sets"); return UNET_ERR_ARG; }
+  for (int i = 0; i < LMAXS; ++i) {
+    ls.z[i] = i < S ? z[i] : nullptr;
+    ls.dz[i] = (i < S && dz) ? dz[i] : nullptr;
+    ls.w[i] = i < S ? (w ? w[i] : 1.f) : 0.f;
+  }
+  return 0;
+}
+
+int unet_loss_reduce_multi(int S, long long N, int K, long long HW, const float* const* z, const int64_t* t,
+                           float* partial, void* stream) {
   if (K < 1 || K > LMAXK) { set_error("unet_loss_reduce: n_classes must be in [1, 16]"); return UNET_ERR_UNSUPPORTED; }
+  LossSets ls;
+  if (int rc = load_sets(S, z, nullptr, nullptr, ls)) return rc;
   const int rows = loss_rows(HW);
   if (K == 2)
-    hipLaunchKernelGGL(loss_reduce_kernel<2>, dim3(rows, N), dim3(256), 0, (hipStream_t)stream, N, K, HW, z, t, partial,
-                       rows);
+    hipLaunchKernelGGL(loss_reduce_kernel<2>, dim3(rows, N, S), dim3(256), 0, (hipStream_t)stream, N, K, HW, ls, t,
+                       partial, rows);
   else
-    hipLaunchKernelGGL(loss_reduce_kernel<0>, dim3(rows, N), dim3(256), 0, (hipStream_t)stream, N, K, HW, z, t, partial,
-                       rows);
+    hipLaunchKernelGGL(loss_reduce_kernel<0>, dim3(rows, N, S), dim3(256), 0, (hipStream_t)stream, N, K, HW, ls, t,
+                       partial, rows);
   return check_launch("loss_reduce");
+}
+
+int unet_loss_reduce(long long N, int K, long long HW, const float* z, const int64_t* t, float* partial, void* stream) {
+  return unet_loss_reduce_multi(1, N, K, HW, &z, t, partial, stream);
+}
+
+int unet_loss_finalize_multi(const float* partial, int rows, int S, const float* set_weights, long long N, int K,
+                             float ce_w, float dice_w, float class_w, float ce_smooth, float dice_smooth, int ignore_bg,
+                             int reduction, float* loss, float* coef, void* stream) {
+  LossSets ls;
+  const float* zs[LMAXS] = {nullptr, nullptr, nullptr, nullptr};
+  if (S < 1 || S > LMAXS || (S > 1 && reduction == 2)) {
+    set_error("unet_loss_finalize: 1 to 4 sets, reduction 'none' only for one set");
+    return UNET_ERR_ARG;
+  }
+  load_sets(S, zs, nullptr, set_weights, ls);
+  const size_t shm = (size_t)(N + N * K + N * (4 + 3 * K)) * sizeof(double);
+  if (shm > 60000) { set_error("unet_loss_finalize: batch too large"); return UNET_ERR_UNSUPPORTED; }
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), shm, (hipStream_t)stream, partial, rows, S, ls, N, K,
+                     ce_w, dice_w, class_w, ce_smooth, dice_smooth, ignore_bg, reduction, loss, coef);
+  return check_launch("loss_finalize");
 }
 
 int unet_loss_finalize(const float* partial, int rows, long long N, int K, float ce_w, float dice_w, float class_w,
                        float ce_smooth, float dice_smooth, int ignore_bg, int reduction, float* loss, float* coef,
                        void* stream) {
-  const size_t shm = (size_t)(N + N * K + N * (4 + 3 * K)) * sizeof(double);
-  if (shm > 60000) { set_error("unet_loss_finalize: batch too large"); return UNET_ERR_UNSUPPORTED; }
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), shm, (hipStream_t)stream, partial, rows, N, K, ce_w,
-                     dice_w, class_w, ce_smooth, dice_smooth, ignore_bg, reduction, loss, coef);
-  return check_launch("loss_finalize");
+  return unet_loss_finalize_multi(partial, rows, 1, nullptr, N, K, ce_w, dice_w, class_w, ce_smooth, dice_smooth,
+                                  ignore_bg, reduction, loss, coef, stream);
+}
+
+int unet_loss_grad_multi(int S, long long N, int K, long long HW, const float* const* z, const int64_t* t,
+                         const float* coef, const float* gout, int gout_per_elem, int ignore_bg, float* const* dz,
+                         void* stream) {
+  LossSets ls;
+  if (!dz) { set_error("unet_loss_grad: no outputs"); return UNET_ERR_ARG; }
+  if (int rc = load_sets(S, z, dz, nullptr, ls)) return rc;
+  long long b = (S * N * HW + 255) / 256;
+  if (b > 8192) b = 8192;
+  const int c_lo = (ignore_bg && K > 1) ? 1 : 0;
+  if (K == 2)
+    hipLaunchKernelGGL(loss_grad_kernel<2>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, S, N, K, HW, ls, t, coef,
+                       gout, gout_per_elem, c_lo);
+  else
+    hipLaunchKernelGGL(loss_grad_kernel<0>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, S, N, K, HW, ls, t, coef,
+                       gout, gout_per_elem, c_lo);
+  return check_launch("loss_grad");
 }
 
 int unet_loss_grad(long long N, int K, long long HW, const float* z, const int64_t* t, const float* coef,
                    const float* gout, int gout_per_elem, int ignore_bg, float* dz, void* stream) {
-  long long b = (N * HW + 255) / 256;
-  if (b > 8192) b = 8192;
-  const int c_lo = (ignore_bg && K > 1) ? 1 : 0;
-  if (K == 2)
-    hipLaunchKernelGGL(loss_grad_kernel<2>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, N, K, HW, z, t, coef, gout,
-                       gout_per_elem, c_lo, dz);
-  else
-    hipLaunchKernelGGL(loss_grad_kernel<0>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, N, K, HW, z, t, coef, gout,
-                       gout_per_elem, c_lo, dz);
-  return check_launch("loss_grad");
+  return unet_loss_grad_multi(1, N, K, HW, &z, t, coef, gout, gout_per_elem, ignore_bg, &dz, stream);
 }
 
 }  // extern "C"

@@ -51,6 +51,46 @@ class _FusedLoss(torch.autograd.Function):
         return dz, None, None, None, None, None, None, None, None
 
 
+class _FusedMultiLoss(torch.autograd.Function):
+    """Σ_s w_s · base(z_s, t) over S same-shape logit sets in one reduce / finalize / grad launch each."""
+
+    @staticmethod
+    def forward(ctx, t, weights, cfg, *zs):
+        ce_w, dice_w, class_w, ce_smooth, dice_smooth, ignore_bg = cfg
+        S = len(zs)
+        N, K, H, W = zs[0].shape
+        zc = [z.detach() if (z.dtype == torch.float32 and z.is_contiguous()) else z.detach().float().contiguous()
+              for z in zs]
+        tc = t if (t.dtype == torch.int64 and t.is_contiguous()) else t.long().contiguous()
+        HW = H * W
+        rows = L.load().unet_loss_rows(HW)
+        dev = zs[0].device
+        part = f32(S, N, rows, 4 + 3 * K, device=dev)
+        zp = (L.c_vp * S)(*[z.data_ptr() for z in zc])
+        L.call("unet_loss_reduce_multi", S, N, K, HW, zp, vp(tc), vp(part), stream())
+        coef = f32(S, N, 2 + 2 * K, device=dev)
+        loss = f32((), device=dev)
+        wts = (L.c_float * S)(*weights)
+        L.call("unet_loss_finalize_multi", vp(part), rows, S, wts, N, K, ce_w, dice_w, class_w, ce_smooth, dice_smooth,
+               int(ignore_bg), 0, vp(loss), vp(coef), stream())
+        ctx.save_for_backward(tc, coef, *zc)
+        ctx.ignore_bg = int(ignore_bg)
+        return loss
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, gout):
+        tc, coef, *zc = ctx.saved_tensors
+        S = len(zc)
+        N, K, H, W = zc[0].shape
+        go = gout.float().contiguous()
+        dz = [torch.empty_like(z) for z in zc]
+        zp = (L.c_vp * S)(*[z.data_ptr() for z in zc])
+        dp = (L.c_vp * S)(*[d.data_ptr() for d in dz])
+        L.call("unet_loss_grad_multi", S, N, K, H * W, zp, vp(tc), vp(coef), vp(go), 0, ctx.ignore_bg, dp, stream())
+        return (None, None, None, *dz)
+
+
 def _fused(z, t, ce_w, dice_w, class_w, ce_smooth=1e-6, dice_smooth=1.0, ignore_bg=True, reduction="mean"):
     require_device(z, "predictions")
     if z.dim() != 4 or t.shape != (z.shape[0], z.shape[2], z.shape[3]):
@@ -102,7 +142,9 @@ class DiceBCELoss(nn.Module):
 
 
 class DeepSupervisionLoss(nn.Module):
-    """Σ_k w_k · base(pred_k, targets) over [main, ds1, ds2, ds3] — reference loss.py:194-229."""
+    """Σ_k w_k · base(pred_k, targets) over [main, ds1, ds2, ds3] — reference loss.py:194-229.
+    With one of the fused bases (DiceBCE / Dice(mean) / BalancedCE) all the sets run through one launch of
+    each loss pass; any other base criterion is applied per set as in the reference."""
 
     def __init__(self, base_criterion: nn.Module, weights: list = None):
         super().__init__()
@@ -111,11 +153,33 @@ class DeepSupervisionLoss(nn.Module):
 
     def forward(self, predictions, targets: torch.Tensor) -> torch.Tensor:
         if isinstance(predictions, (list, tuple)):
+            cfg = _fused_cfg(self.base_criterion)
+            n = min(len(predictions), len(self.weights))
+            if (cfg is not None and 1 <= n <= 4 and all(p.dim() == 4 and p.shape == predictions[0].shape
+                                                        for p in predictions[:n])):
+                # the four logit sets through one reduce / finalize / grad launch (unet_loss_*_multi)
+                require_device(predictions[0], "predictions")
+                if targets.shape != (predictions[0].shape[0], predictions[0].shape[2], predictions[0].shape[3]):
+                    raise RuntimeError(f"expected targets (N, H, W), got {tuple(targets.shape)}")
+                return _FusedMultiLoss.apply(targets, [float(w) for w in self.weights[:n]], cfg,
+                                             *predictions[:n])
             total = 0.0
             for pred, w in zip(predictions, self.weights):
                 total = total + w * self.base_criterion(pred, targets)
             return total
         return self.base_criterion(predictions, targets)
+
+
+def _fused_cfg(crit: nn.Module):
+    """(ce_w, dice_w, class_w, ce_smooth, dice_smooth, ignore_bg) of a mean-reduced fused loss, else None."""
+    if type(crit) is DiceBCELoss:
+        return (float(crit.ce_weight), float(crit.dice_weight), float(crit.balanced_ce.class_weight),
+                float(crit.balanced_ce.smooth), float(crit.dice_loss.smooth), bool(crit.dice_loss.ignore_background))
+    if type(crit) is DiceLoss and crit.reduction == "mean":
+        return (0.0, 1.0, 0.5, 1e-6, float(crit.smooth), bool(crit.ignore_background))
+    if type(crit) is BalancedCELoss:
+        return (1.0, 0.0, float(crit.class_weight), float(crit.smooth), 1.0, True)
+    return None
 
 
 def create_loss_function(loss_type: str = "dice_bce", ce_weight: float = 1.0, dice_weight: float = 1.0,
