@@ -262,6 +262,26 @@ int unet_loss_grad_multi(int S, long long N, int K, long long HW, const float* c
                          const float* coef, const float* gout, int gout_per_elem, int ignore_bg, float* const* dz,
                          void* stream);
 
+/* ---- device input pipeline and inference post-processing (csrc/infer.hip) ------------------- */
+/* One separable pass of PIL's 8-bit Image.resize(BILINEAR) (Resample.c) over a (N, inH, inW) uint8
+ * batch: axis 1 = horizontal (out (N, inH, out_len)), axis 0 = vertical (out (N, out_len, inW)).
+ * bounds int32 [out_len][2] (first source index, count) and coeffs int32 [out_len][ksize] are
+ * Pillow's fixed-point tables (unet/utils/pil_tables.py).  roundtrip != 0 first maps each source
+ * byte u -> uint8(float32(u / 255) * 255) (the float round trip of augmentations.py:150).           */
+int unet_resample_u8(int axis, long long N, int inH, int inW, int out_len, const uint8_t* in, int roundtrip,
+                     const int32_t* bounds, const int32_t* coeffs, int ksize, uint8_t* out, void* stream);
+/* apply_basic_transforms tail (augmentations.py:153-171) + mask binarisation (dataset.py:148-149):
+ * out_img fp32 (N,1,H,W) = (uint8 img [after the optional round trip] / 255 - mean) / std, flipped
+ * left-right where flip[n] != 0 (flip may be NULL); if mask != NULL: out_mask int64 (N,H,W) =
+ * (mask[n][ytab[y]][xtab[x']] > 127) with PIL NEAREST tables ytab[H], xtab[W] (mask is mask_h x mask_w). */
+int unet_slice_finish(long long N, int H, int W, const uint8_t* img, int roundtrip, int mask_h, int mask_w,
+                      const uint8_t* mask, const int32_t* ytab, const int32_t* xtab, const uint8_t* flip, float mean,
+                      float stdv, float* out_img, int64_t* out_mask, void* stream);
+/* postprocess_mask of scripts/predict.py:138-165: out uint8 (N,outH,outW) = 255 where
+ * softmax(logits[n, :, ytab[y], xtab[x]])[cls] > threshold, else 0 (PIL NEAREST tables).           */
+int unet_postprocess_mask(long long N, int K, int H, int W, const float* logits, int cls, float threshold, int outH,
+                          int outW, const int32_t* ytab, const int32_t* xtab, uint8_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

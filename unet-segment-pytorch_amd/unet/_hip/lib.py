@@ -102,6 +102,11 @@ _SIGS = {
     "unet_loss_finalize": (c_int, [c_vp, c_int, c_ll, c_int, c_float, c_float, c_float, c_float, c_float, c_int, c_int,
                                    c_vp, c_vp, c_vp]),
     "unet_loss_grad": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
+    "unet_resample_u8": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "unet_slice_finish": (c_int, [c_ll, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_float,
+                                  c_float, c_vp, c_vp, c_vp]),
+    "unet_postprocess_mask": (c_int, [c_ll, c_int, c_int, c_int, c_vp, c_int, c_float, c_int, c_int, c_vp, c_vp, c_vp,
+                                      c_vp]),
     "unet_loss_reduce_multi": (c_int, [c_int, c_ll, c_int, c_ll, ctypes.POINTER(c_vp), c_vp, c_vp, c_vp]),
     "unet_loss_finalize_multi": (c_int, [c_vp, c_int, c_int, ctypes.POINTER(c_float), c_ll, c_int, c_float, c_float,
                                          c_float, c_float, c_float, c_int, c_int, c_vp, c_vp, c_vp]),
