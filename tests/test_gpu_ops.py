@@ -641,3 +641,54 @@ def test_wgrad_bench_sizes(shape):
     torch.cuda.synchronize()
     rel = float((dw - ref).double().norm() / ref.double().norm())
     assert rel <= 1e-4, rel     # fp32 accumulation of exact bf16 products: only the summation order differs
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 128, 64, 128), (2, 66, 70, 128, 64), (4, 256, 256, 128, 64)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("kind", ["plain", "act", "gated+plain"])
+def test_wgrad_source_kinds(shape, kind):
+    """wgrad2's compile-time source-kind staging (plain map / BN+ReLU source / the up-block concat of a
+    gated skip and the stored upsampled map) vs torch's conv2d_weight on the same activation."""
+    L, R = _lib(), _rt()
+    N, H, W, cin, cout = shape
+    dt = torch.bfloat16
+    torch.manual_seed(16)
+    dy = _rand(N, H, W, cout, dt=dt)
+    if kind == "plain":
+        y = _rand(N, H, W, cin, dt=dt)
+        src = L.Src()
+        src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cin, H, W, y.data_ptr()
+        srcs, x = [src], y.float()
+    elif kind == "act":
+        y = _rand(N, H, W, cin, dt=dt)
+        ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
+        srcs, x = [_act_src(y, ab)], _act_ref(y, ab).to(dt).float()
+    else:
+        cs = cin // 2
+        skip = _rand(N, H, W, cs, dt=dt)
+        ab = torch.stack([torch.rand(cs, device="cuda") + 0.5, torch.randn(cs, device="cuda") * 0.2])
+        p = torch.randn(N, H, W, device="cuda")
+        pab = torch.tensor([0.7, -0.1], device="cuda")
+        s0 = _act_src(skip, ab)
+        s0.gate_p, s0.gate_ab = p.data_ptr(), pab.data_ptr()
+        up = _rand(N, H, W, cin - cs, dt=dt)
+        s1 = L.Src()
+        s1.kind, s1.C, s1.H, s1.W, s1.data = L.SRC_PLAIN, cin - cs, H, W, up.data_ptr()
+        xs = _act_ref(skip, ab) * torch.sigmoid(p * 0.7 - 0.1)[..., None]
+        srcs, x = [s0, s1], torch.cat([xs.to(dt).float(), up.float()], -1)
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2), (cout, cin, 3, 3), dy.float().permute(0, 3, 1, 2),
+                                      padding=1)
+    wd = L.WgradDesc()
+    wd.dtype = R.BF16.code
+    wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = N, H, W, cin, cout, 3, len(srcs)
+    for i, s in enumerate(srcs):
+        wd.src[i] = s
+    wd.dy = dy.data_ptr()
+    dw = torch.empty(cout, cin, 3, 3, device="cuda")
+    wd.dw = dw.data_ptr()
+    ws = torch.empty(max(L.load().unet_wgrad_workspace(wd), 16), dtype=torch.uint8, device="cuda")
+    wd.workspace = ws.data_ptr()
+    L.call("unet_conv_wgrad", wd, R.stream())
+    torch.cuda.synchronize()
+    rel = float((dw - ref).double().norm() / ref.double().norm())
+    assert rel <= 2e-3, rel    # the gate / activation rounding to bf16 can differ by one ulp from torch's

@@ -25,12 +25,29 @@ int slab_reduce_two_pass(const float* ws, int splits, long long total, float* sc
 __device__ __forceinline__ bf16x8 tr8(const bf16* r0, const bf16* r1) {
   const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r0));
   const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r1));
-  typedef __attribute__((ext_vector_type(8))) short i16x8;
-  const i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, r);
+  // one vector concatenation (lets the two reads land in the halves of one register quad; an element-wise
+  // initialiser compiled to v_mov copies)
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-template <int KS, int WCO, int WCI, int MI, int RAW>
+// compile-time source kinds of the conv input (as conv3's SK): W2_ANY switches per halo item at run time;
+// W2_PLAIN: stored map(s) only; W2_ACT: BN(+ReLU)(+gate) source(s) and stored ones, decided per thread
+// (a thread's channel vector has one source).  Known kinds keep only that staging code: a plain vector
+// goes to LDS as loaded, an activated one is unpacked, transformed and packed once.
+enum { W2_ANY = 0, W2_PLAIN = 1, W2_ACT = 2 };
+
+__device__ __forceinline__ uint4 pack8(const float* v) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  unsigned u[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16x2 p = {(__bf16)v[2 * i], (__bf16)v[2 * i + 1]};
+    u[i] = __builtin_bit_cast(unsigned, p);
+  }
+  return make_uint4(u[0], u[1], u[2], u[3]);
+}
+
+template <int KS, int WCO, int WCI, int MI, int RAW, int SK = W2_ANY>
 __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad_desc d, int tiles_w, int tiles_h, int mtiles,
                                                       int per_split, float* ws) {
   using T = bf16;
@@ -82,30 +99,54 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
   // staging of a tile, split into pieces so that only a few raw loads are in flight at once:
   //   dy vectors: issued at K-step 0, stored after K-step 1; halo item k: issued at K-step
   //   (3k / IX), stored after the following K-step (see the main loop)
-  Item<RAW> xi[IX];
+  Item<SK == W2_ANY ? RAW : 1> xi[SK == W2_ANY ? IX : 1];
   uint4 dq[ID];
-  auto issue_x = [&](int mt, int k) {
-    long long n;
-    int h0, w0;
-    tile_nhw(mt, n, h0, w0);
+  // SK != W2_ANY: raw 16-byte vectors (zero outside the map), the gate pre-activation per item
+  const bool act_src = SK == W2_ACT && (sv.kind == UNET_SRC_ACT);
+  uint4 xq[IX];
+  float xg[IX];
+  auto issue_x = [&](long long n, int h0, int w0, int k) {
     const int hp = (tid + k * W2_NT) / NVX;
-    item_issue<T, RAW>(sv, d.H, d.W, n, h0 + hp / HWID - HALO, w0 + hp % HWID - HALO, hp < HP, xi[k]);
-  };
-  auto finish_x = [&](int mt, int k, T* buf) {
-    long long n;
-    int h0, w0;
-    tile_nhw(mt, n, h0, w0);
-    const int hp = (tid + k * W2_NT) / NVX;
-    if (hp < HP) {
-      float vals[VEC];
-      item_finish<T, RAW>(d, sv, sc, sf, n, h0 + hp / HWID - HALO, w0 + hp % HWID - HALO, ci0 + vx * VEC, xi[k], vals);
-      store_vec<T>(buf + hp * RSX + vx * VEC, vals);
+    const int y = h0 + hp / HWID - HALO, x = w0 + hp % HWID - HALO;
+    if constexpr (SK == W2_ANY) {
+      item_issue<T, RAW>(sv, d.H, d.W, n, y, x, hp < HP, xi[k]);
+    } else {
+      xq[k] = make_uint4(0, 0, 0, 0);
+      xg[k] = 0.f;
+      if (hp < HP && sv.fast && y >= 0 && y < d.H && x >= 0 && x < d.W) {
+        const unsigned px = ((unsigned)n * d.H + y) * d.W + x;
+        xq[k] = ld16b(sv.base, px * sv.pixb);
+        if (act_src && sv.gate_p) xg[k] = sv.gate_p[px];
+      }
     }
   };
-  auto issue_d = [&](int mt) {
-    long long n;
-    int h0, w0;
-    tile_nhw(mt, n, h0, w0);
+  auto finish_x = [&](long long n, int h0, int w0, int k, T* buf) {
+    const int hp = (tid + k * W2_NT) / NVX;
+    if (hp < HP) {
+      if constexpr (SK == W2_ANY) {
+        float vals[VEC];
+        item_finish<T, RAW>(d, sv, sc, sf, n, h0 + hp / HWID - HALO, w0 + hp % HWID - HALO, ci0 + vx * VEC, xi[k],
+                            vals);
+        store_vec<T>(buf + hp * RSX + vx * VEC, vals);
+      } else {
+        uint4 o = xq[k];
+        if (act_src) {
+          // zero-padding positions stay zero (the conv pads the activation, not y)
+          const int y = h0 + hp / HWID - HALO, x = w0 + hp % HWID - HALO;
+          const bool inb = sv.fast && y >= 0 && y < d.H && x >= 0 && x < d.W;
+          float v[VEC];
+          unpack16<T>(o, v);
+          const float lo = sv.relu ? 0.f : -INFINITY;
+          const float gm = sv.gate_p ? sigmoidf_(xg[k] * sv.gate_ab[0] + sv.gate_ab[1]) : 1.f;
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) v[j] = inb ? fmaxf(v[j] * sc[j] + sf[j], lo) * gm : 0.f;
+          o = pack8(v);
+        }
+        *reinterpret_cast<uint4*>(buf + hp * RSX + vx * VEC) = o;
+      }
+    }
+  };
+  auto issue_d = [&](long long n, int h0, int w0) {
 #pragma unroll
     for (int k = 0; k < ID; ++k) {
       const int p = (tid + k * W2_NT) / NVD;
@@ -124,14 +165,14 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
       if (p < W2_BM) *reinterpret_cast<uint4*>(bd + (p ^ ((p & 8) >> 1)) * RSD + vd * VEC) = dq[k];
     }
   };
-  auto issue = [&](int mt) {
+  auto issue = [&](long long n, int h0, int w0) {
 #pragma unroll
-    for (int k = 0; k < IX; ++k) issue_x(mt, k);
-    issue_d(mt);
+    for (int k = 0; k < IX; ++k) issue_x(n, h0, w0, k);
+    issue_d(n, h0, w0);
   };
-  auto finish = [&](int mt, T* buf) {
+  auto finish = [&](long long n, int h0, int w0, T* buf) {
 #pragma unroll
-    for (int k = 0; k < IX; ++k) finish_x(mt, k, buf);
+    for (int k = 0; k < IX; ++k) finish_x(n, h0, w0, k, buf);
     finish_d(buf);
   };
 
@@ -142,8 +183,11 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
     for (int i = 0; i < MI; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (mt_begin < mt_end) {
-    issue(mt_begin);
-    finish(mt_begin, lds);
+    long long n;
+    int h0, w0;
+    tile_nhw(mt_begin, n, h0, w0);
+    issue(n, h0, w0);
+    finish(n, h0, w0, lds);
   }
   __syncthreads();
 
@@ -154,6 +198,9 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
     const T* bd = bx + HP * RSX;
     const bool has_next = mt + 1 < mt_end;
     T* nb = lds + (cur ^ 1) * BUF;
+    long long nn = 0;   // the next tile's coordinates, once per tile
+    int nh0 = 0, nw0 = 0;
+    if (has_next) tile_nhw(mt + 1, nn, nh0, nw0);
 #pragma unroll
     for (int k0 = 0; k0 < W2_BM; k0 += 32) {
       const int s = k0 / 32;  // K step 0..3
@@ -165,14 +212,14 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
         if constexpr (RAW == 1) {
           if (s == 0) {
 #pragma unroll
-            for (int k = 0; k < IX; ++k) issue_x(mt + 1, k);
+            for (int k = 0; k < IX; ++k) issue_x(nn, nh0, nw0, k);
           }
-          if (s == 1) issue_d(mt + 1);
+          if (s == 1) issue_d(nn, nh0, nw0);
         } else {
-          if (s == 0) issue_d(mt + 1);
+          if (s == 0) issue_d(nn, nh0, nw0);
 #pragma unroll
           for (int k = 0; k < IX; ++k)
-            if ((3 * k) / IX == s) issue_x(mt + 1, k);
+            if ((3 * k) / IX == s) issue_x(nn, nh0, nw0, k);
         }
       }
       // lane bases + compile-time offsets (so every LDS read is base + immediate): this lane addresses
@@ -199,13 +246,13 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
         if constexpr (RAW == 1) {
 #pragma unroll
           for (int k = 0; k < IX; ++k)
-            if (s == 2 + (k * 2) / IX) finish_x(mt + 1, k, nb);
+            if (s == 2 + (k * 2) / IX) finish_x(nn, nh0, nw0, k, nb);
           if (s == 3) finish_d(nb);
         } else {
           if (s == 1) finish_d(nb);
 #pragma unroll
           for (int k = 0; k < IX; ++k)
-            if ((3 * k) / IX + 1 == s) finish_x(mt + 1, k, nb);
+            if ((3 * k) / IX + 1 == s) finish_x(nn, nh0, nw0, k, nb);
         }
       }
     }
@@ -215,15 +262,20 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
   // slab (OIHW order): ws[split][co][ci][tap]; C layout: row (co) = 4*(l>>4)+r, col (ci) = l&15
   float* slab = ws + (size_t)split * d.Cout * d.Cin * TAPS;
   const int ci = ci0 + wci * 16 + (lane & 15);
+  const int cob = co0 + wco * 16 * MI + 4 * (lane >> 4);
+  const unsigned row = (unsigned)d.Cin * TAPS;   // slab elements per output channel
+  const unsigned base = ((unsigned)cob * d.Cin + ci) * TAPS;
 #pragma unroll
-  for (int t = 0; t < TAPS; ++t)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int r = 0; r < 4; ++r) {
+      const int co = cob + i * 16 + r;
+      if (co < d.Cout && ci < d.Cin) {
+        float* o = slab + base + (unsigned)(i * 16 + r) * row;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco * 16 * MI + i * 16 + 4 * (lane >> 4) + r;
-        if (co < d.Cout && ci < d.Cin) slab[((size_t)co * d.Cin + ci) * TAPS + t] = acc[t][i][r];
+        for (int t = 0; t < TAPS; ++t) o[t] = acc[t][i][r];
       }
+    }
 }
 
 // dw (+)= Σ_s ws[s]   (fixed order; 16-byte accesses when the size allows)
@@ -308,20 +360,40 @@ W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   return p;
 }
 
-template <int KS, int WCO, int WCI, int MI, int RAW>
+template <int KS, int WCO, int WCI, int MI, int RAW, int SK = W2_ANY>
 static int launch_w2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
   dim3 grid(p.splits, cdiv(d->Cin, WCI * 16), cdiv(d->Cout, WCO * 16 * MI));
-  hipLaunchKernelGGL((wgrad2_kernel<KS, WCO, WCI, MI, RAW>), grid, dim3(64 * WCO * WCI), 0, st, *d, p.tiles_w, p.tiles_h, p.mtiles,
+  hipLaunchKernelGGL((wgrad2_kernel<KS, WCO, WCI, MI, RAW, SK>), grid, dim3(64 * WCO * WCI), 0, st, *d, p.tiles_w, p.tiles_h, p.mtiles,
                      p.per_split, (float*)d->workspace);
   return check_launch("wgrad2");
+}
+
+// the W2 source-kind specialisation a raw-1 descriptor can use
+static int w2_source_kinds(const unet_wgrad_desc* d) {
+  bool plain = true, ok = true;
+  for (int i = 0; i < d->nsrc; ++i) {
+    const unet_src& s = d->src[i];
+    if (s.kind == UNET_SRC_ACT) plain = false;
+    else if (s.kind != UNET_SRC_PLAIN || s.gate_p) ok = false;
+  }
+  return !ok ? W2_ANY : (plain ? W2_PLAIN : W2_ACT);
 }
 
 template <int KS, int RAW>
 static int launch_w2_cfg(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
   if (p.wco == 1) return launch_w2<KS, 1, 4, 4, RAW>(d, p, st);
   if constexpr (KS == 3 && RAW == 1) {
-    if (p.wco == 4) return launch_w2<KS, 4, 2, 2, RAW>(d, p, st);
-    if (p.wco == 2 && p.mi == 2) return launch_w2<KS, 2, 4, 2, RAW>(d, p, st);
+    const int sk = w2_source_kinds(d);
+    if (p.wco == 4) {
+      if (sk == W2_PLAIN) return launch_w2<KS, 4, 2, 2, RAW, W2_PLAIN>(d, p, st);
+      if (sk == W2_ACT) return launch_w2<KS, 4, 2, 2, RAW, W2_ACT>(d, p, st);
+      return launch_w2<KS, 4, 2, 2, RAW>(d, p, st);
+    }
+    if (p.wco == 2 && p.mi == 2) {
+      if (sk == W2_PLAIN) return launch_w2<KS, 2, 4, 2, RAW, W2_PLAIN>(d, p, st);
+      if (sk == W2_ACT) return launch_w2<KS, 2, 4, 2, RAW, W2_ACT>(d, p, st);
+      return launch_w2<KS, 2, 4, 2, RAW>(d, p, st);
+    }
   }
   if constexpr (KS == 1) {
     if (p.wci == 4) return launch_w2<KS, 2, 4, 4, RAW>(d, p, st);
