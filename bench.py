@@ -30,9 +30,21 @@ sys.path.insert(0, str(ROOT / "unet-segment-pytorch_amd"))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense peaks (MI355X_MICROARCH.md)
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}   # MI355X dense peaks (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 FLOPS_PER_IMAGE = {"attention_unet": 983.4e9, "unet": 957.5e9}   # fwd+bwd, 1ch 512^2
+FLOPS_PER_IMAGE_C5 = 3938.3e9                                      # AttentionUNet 3ch 1024^2 fwd+bwd
+METRIC = "512x512 CT slices/sec fwd+bwd, AttentionUNet bs=4/GPU, 1/2/4/8 MI355X"   # BASELINE.json
+
+
+def cpu_model() -> str:
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def disc_targets(n: int, h: int, w: int, gen: torch.Generator) -> torch.Tensor:
@@ -73,7 +85,7 @@ def cpu_baseline(model_kind: str, size: int, batch: int, iters: int) -> dict:
         one()
     dt = time.perf_counter() - t0
     return {"value": round(batch * iters / dt, 4), "unit": "img/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "kind": "port",
             "sample": f"oracle/unet_oracle.py fp32 CPU, {model_kind} 1x{size}x{size}, batch {batch}, "
                       f"1 warm-up + {iters} timed fwd+DiceBCE+bwd iterations ({dt:.1f} s)"}
 
@@ -97,12 +109,15 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--in-ch", type=int, default=1, help="input channels (C5: 3)")
     ap.add_argument("--accum", type=int, default=1, help="micro-batches per optimizer step (C5: 8; scripts/train.py:133-143)")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="operand type; fp16 adds dynamic loss scaling (torch.amp.GradScaler), as C5 asks")
     ap.add_argument("--probe", default=None, help="kernel family to time live (default: conv_kernel<prec,3,64>)")
     ap.add_argument("--bucket-mb", type=float, default=25.0, help="DDP bucket_cap_mb (N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=2)
-    ap.add_argument("--cpu-batch", type=int, default=1)
+    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--no-fp32-line", action="store_true",
+                    help="skip the fp32-operand (reference numerics) rate reported beside a 16-bit run at N=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,6 +151,9 @@ def main():
         net = wrap_ddp(model, local if backend == "nccl" else None, bucket_cap_mb=args.bucket_mb,
                        broadcast_buffers=False)
     opt = torch.optim.AdamW(model.parameters(), lr=5e-5, weight_decay=1e-4, fused=True)
+    # fp16 operands: dynamic loss scaling as torch.amp prescribes for fp16 training (SURVEY §5 mixed
+    # precision); gradients are unscaled before the clip (scripts/train.py:136-141 order)
+    scaler = torch.amp.GradScaler("cuda", enabled=args.precision == "fp16")
     crit = DiceBCELoss()
     gen = torch.Generator().manual_seed(1234 + rank)
     x = (torch.rand(args.batch, args.in_ch, args.size, args.size, generator=gen) * 2 - 1).to(dev)
@@ -150,30 +168,38 @@ def main():
             ctx = net.no_sync() if (world > 1 and not last) else contextlib.nullcontext()
             with ctx:
                 loss = crit(net(x), t)
-                (loss / args.accum if args.accum > 1 else loss).backward()
+                scaler.scale(loss / args.accum if args.accum > 1 else loss).backward()
+        scaler.unscale_(opt)
         torch.nn.utils.clip_grad_norm_(params, 1.0)
-        opt.step()
+        scaler.step(opt)
+        scaler.update()
         opt.zero_grad(set_to_none=True)
         return loss
 
+    def timed(fn, steps):
+        """barrier + synchronize on both sides; the slowest rank's wall time"""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return max_over_ranks(time.perf_counter() - t0, dev), out
+
     for _ in range(args.warmup):
         step()
-    # the dominant kernel: every bf16 3x3 conv launch (fwd + dgrad; all tile instantiations of conv3_kernel,
-    # prefix match), ~44 % of the step
-    target = args.probe or ("conv3_kernel<bf16,3," if args.precision == "bf16" else "conv2_kernel<fp32,3,")
+    elapsed, loss = timed(step, args.steps)          # the headline: no probe events inside
+
+    # the dominant kernel, timed live in a separate pass of the same steps: every 16-bit 3x3 conv launch
+    # (fwd + dgrad; all tile instantiations of conv3_kernel, prefix match), ~44 % of the step
+    tn = {"bf16": "bf16", "fp16": "fp16"}.get(args.precision)
+    target = args.probe or (f"conv3_kernel<{tn},3," if tn else "conv2_kernel<fp32,3,")
     probe.enable(target)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    timed(step, max(2, min(args.steps, 10)))
     probe.disable()
-    elapsed = max_over_ranks(elapsed, dev)
     ps = probe.summary()
 
     # SURVEY §8(d) also asks for the rate without the optimizer: the same fwd + loss + bwd (+ gradient
@@ -184,20 +210,11 @@ def main():
             ctx = net.no_sync() if (world > 1 and not last) else contextlib.nullcontext()
             with ctx:
                 l = crit(net(x), t)
-                (l / args.accum if args.accum > 1 else l).backward()
+                scaler.scale(l / args.accum if args.accum > 1 else l).backward()
         opt.zero_grad(set_to_none=True)
 
     fwd_bwd()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        fwd_bwd()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el_nb = max_over_ranks(time.perf_counter() - t1, dev)
+    el_nb, _ = timed(fwd_bwd, args.steps)
 
     images = world * args.batch * args.accum * args.steps
     value = images / elapsed
@@ -209,29 +226,47 @@ def main():
         tr = json.loads(tfile.read_text())
         ent = tr.get(target)
         traffic = ent.get("bytes_per_launch") if isinstance(ent, dict) else ent
+    headline = (args.size, args.in_ch, args.accum) == (512, 1, 1)
+    metric = METRIC if headline else (
+        f"{args.size}x{args.size} {args.in_ch}-ch slices/sec fwd+bwd, {'AttentionUNet' if args.model == 'attention_unet' else 'UNet'} "
+        f"bs={args.batch}/GPU x grad-accum {args.accum}, {args.precision}, 1/2/4/8 MI355X")
+    fpi = FLOPS_PER_IMAGE[args.model] if (args.size, args.in_ch) == (512, 1) else (
+        FLOPS_PER_IMAGE_C5 if (args.size, args.in_ch, args.model) == (1024, 3, "attention_unet") else None)
     line = {
-        "metric": "512x512 CT slices/sec fwd+bwd, AttentionUNet bs=4/GPU, 1/2/4/8 MI355X",
+        "metric": metric,
         "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.precision, "data": "synthetic (x~U(-1,1), 1-3 disc masks/img; seeded)",
         "config": {"workload": f"{args.model} {args.in_ch}x{args.size}x{args.size} train step "
-                               f"(fwd+DiceBCE+bwd{' x%d accum' % args.accum if args.accum > 1 else ''}+clip+AdamW)",
+                               f"(fwd+DiceBCE+bwd{' x%d accum' % args.accum if args.accum > 1 else ''}+clip+AdamW"
+                               f"{'; GradScaler' if scaler.is_enabled() else ''})",
                    "model": args.model, "global_batch": world * args.batch * args.accum, "per_gpu_batch": args.batch,
                    "grad_accum": args.accum, "image": [args.in_ch, args.size, args.size],
                    "parallelism": f"dp{world}" if world > 1 else "single",
                    "grad_sync": f"torch DDP ({backend}, bucket {args.bucket_mb:g} MB)" if world > 1 else None},
-        "whole_step_tflops": (round(value * FLOPS_PER_IMAGE[args.model] / 1e12, 2)
-                              if (args.size, args.in_ch) == (512, 1) else None),
+        "whole_step_tflops": round(value * fpi / 1e12, 2) if fpi else None,
         "roofline": {"kernel": target, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_unit": "HBM bytes/launch (rocprofv3 PMC, profiles/traffic.json)",
                      "launches": ps["launches"], "avg_us": round(ps["avg_us"], 2) if ps["avg_us"] else None,
-                     "flops_per_launch": round(ps["flops"] / ps["launches"]) if ps["launches"] else None},
+                     "flops_per_launch": round(ps["flops"] / ps["launches"]) if ps["launches"] else None,
+                     "timed": "separate probe pass (HIP events on the launch stream), not the headline loop"},
         "final_loss": round(float(loss.detach()), 5),
         "without_optimizer": {"value": round(world * args.batch * args.accum * args.steps / el_nb, 3),
                               "ms_per_step": round(el_nb / args.steps * 1e3, 3),
                               "note": "fwd+DiceBCE+bwd (+grad averaging), no clip/AdamW"},
     }
+    if scaler.is_enabled():
+        line["loss_scale"] = float(scaler.get_scale())
+    if world == 1 and args.precision != "fp32" and not args.no_fp32_line:
+        # the same step with fp32 operands (the reference's numerics; what the parity tests pin)
+        model.hip_precision = "fp32"
+        scaler = torch.amp.GradScaler("cuda", enabled=False)
+        step()
+        n32 = max(2, min(args.steps, 5))
+        el32, _ = timed(step, n32)
+        line["fp32_operands"] = {"value": round(args.batch * args.accum * n32 / el32, 3),
+                                 "ms_per_step": round(el32 / n32 * 1e3, 3), "steps": n32}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.model, args.size, args.cpu_batch, args.cpu_iters)
     if rank == 0:

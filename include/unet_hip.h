@@ -9,7 +9,7 @@
  *
  * Conventions
  *  - Plain pointers + sizes only.  Activations are NHWC (channels innermost), element type chosen by
- *    `dtype` (UNET_F32 or UNET_BF16); BN statistics, gradients and parameters are fp32.
+ *    `dtype` (UNET_F32, UNET_BF16 or UNET_F16); BN statistics, gradients and parameters are fp32.
  *  - `stream` is a hipStream_t passed as void* (0 = legacy default stream).  No entry point
  *    synchronises, allocates, or reads device memory from the host.
  *  - Every entry point returns 0 on success or a hipError_t / UNET_ERR_* code; unet_last_error()
@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-enum { UNET_F32 = 0, UNET_BF16 = 1 };
+enum { UNET_F32 = 0, UNET_BF16 = 1, UNET_F16 = 2 };  /* operand (activation / weight) type */
 enum { UNET_ERR_ARG = 1001, UNET_ERR_UNSUPPORTED = 1002 };
 
 /* How a convolution input channel range is produced from a stored tensor ("virtual activation").

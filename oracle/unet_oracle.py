@@ -20,6 +20,7 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -198,6 +199,26 @@ def confusion_matrix(pred_labels: torch.Tensor, t: torch.Tensor, num_classes: in
     """SegmentationMetrics.update — metrics.py:55-84 (bincount form of the per-pixel loop)."""
     k = t.reshape(-1).long() * num_classes + pred_labels.reshape(-1).long()
     return torch.bincount(k, minlength=num_classes * num_classes).reshape(num_classes, num_classes)
+
+
+def segmentation_scores(cm: np.ndarray, class_names) -> dict:
+    """SegmentationMetrics.compute — metrics.py:86-143: per class c, tp = cm[c, c], fp = column c minus tp,
+    fn = row c minus tp; IoU = tp / (tp + fp + fn), Dice = 2 tp / (2 tp + fp + fn) (0 for a zero
+    denominator); means over the classes whose score is non-zero; all zeros for an empty matrix."""
+    total = cm.sum()
+    iou, dice = {}, {}
+    for c, name in enumerate(class_names):
+        tp = cm[c, c]
+        fp = cm[:, c].sum() - tp
+        fn = cm[c, :].sum() - tp
+        iou[name] = float(tp / (tp + fp + fn)) if total and tp + fp + fn > 0 else 0.0
+        dice[name] = float(2 * tp / (2 * tp + fp + fn)) if total and 2 * tp + fp + fn > 0 else 0.0
+    vi = [v for v in iou.values() if v > 0]
+    vd = [v for v in dice.values() if v > 0]
+    return {"pixel_accuracy": float(np.trace(cm) / total) if total else 0.0,
+            "mean_iou": float(np.mean(vi)) if vi and total else 0.0,
+            "mean_dice": float(np.mean(vd)) if vd and total else 0.0,
+            "class_iou": iou, "class_dice": dice}
 
 
 def tumor_dice(pred_labels: torch.Tensor, t: torch.Tensor) -> float:

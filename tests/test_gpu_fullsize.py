@@ -12,7 +12,7 @@ Gates:
   matrix (device kernel on our logits) equal to the oracle's up to those pixels; loss within 1e-5 rel;
   BN running buffers within 1e-4; eval-mode logits within 1e-4 (1 + max).  Parameter gradients against
   the fp64 oracle: no worse than 1.5x the CPU fp32 oracle's own error.
-  bf16 operand mode — see test_fullsize_bf16_vs_oracle: no worse than PyTorch's own bf16 execution.
+  bf16 / fp16 operand modes — see test_fullsize_16bit_vs_oracle: no worse than PyTorch's own 16-bit execution.
 """
 
 import os
@@ -40,7 +40,8 @@ def _discs(n, h, w, gen):
 
 def _oracle(init, x, t, dev, dtype, autocast=False):
     """The oracle's fwd + DiceBCE + bwd with the parameters/buffers of `init` on `dev` in `dtype`
-    (autocast=True: the reference's network under torch.autocast(bf16), i.e. PyTorch's own bf16 run)."""
+    (autocast=True / a 16-bit dtype: the reference's network under torch.autocast(bf16 / that dtype),
+    i.e. PyTorch's own 16-bit run)."""
     from oracle import unet_oracle as O
     p = {}
     for k, v in init.items():
@@ -52,7 +53,7 @@ def _oracle(init, x, t, dev, dtype, autocast=False):
         p[k] = v
     xx = x.to(dev, dtype)
     if autocast:
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16 if autocast is True else autocast):
             out = O.attention_unet_forward(p, xx, training=True)
         out = out.float()
     else:
@@ -179,7 +180,8 @@ def _bf16_report(name, out, loss, grads, f64):
     return e, agree, lrel, r
 
 
-def test_fullsize_bf16_vs_oracle(full_ref):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_fullsize_16bit_vs_oracle(full_ref, prec):
     """bf16 operand mode at the bench configuration, against the fp64 oracle, beside PyTorch's own bf16
     execution of the reference network (torch.autocast on the GPU) on the same weights and batch.
     SURVEY §8(d) proposed rel-L2 <= 1e-2 on the logits; measured here, autocast-bf16 itself is at ~0.14
@@ -187,16 +189,18 @@ def test_fullsize_bf16_vs_oracle(full_ref):
     rounding (it is not a kernel error: the fp32 mode of the same kernels is at 2e-5).  The gate is
     therefore: no worse than PyTorch's bf16 (logits rel-L2 and gradient rel-L2 within 1.1x + small,
     argmax agreement within 0.5 %), loss within 1e-2 rel (measured ~1e-3), plus absolute ceilings."""
-    ref, f64, ac = full_ref, full_ref["f64"], full_ref["ac16"]
+    ref, f64 = full_ref, full_ref["f64"]
+    ac = full_ref["ac16"] if prec == "bf16" else _oracle(ref["init"], ref["x"], ref["t"], "cuda", torch.float32,
+                                                         autocast=torch.float16)
     log = []
-    m, out, loss = _run(ref, "bf16", log)
+    m, out, loss = _run(ref, prec, log)
     ran = set(log)
-    missing = BENCH_CONV3 - ran
+    missing = {(k.replace("bf16", prec), mode) for k, mode in BENCH_CONV3} - ran
     assert not missing, (missing, sorted(ran))
     grads = {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()}
     print()
-    e, agree, lrel, r = _bf16_report("bf16 HIP      ", out, loss, grads, f64)
-    e_a, agree_a, lrel_a, r_a = _bf16_report("bf16 autocast ", ac["out"], ac["loss"], ac["grads"], f64)
+    e, agree, lrel, r = _bf16_report(f"{prec} HIP      ", out, loss, grads, f64)
+    e_a, agree_a, lrel_a, r_a = _bf16_report(f"{prec} autocast ", ac["out"], ac["loss"], ac["grads"], f64)
     assert e <= 1.1 * e_a + 5e-3 and e <= 0.2, (e, e_a)
     assert agree >= agree_a - 5e-3 and agree >= 0.95, (agree, agree_a)
     assert lrel <= 1e-2, lrel
@@ -206,5 +210,5 @@ def test_fullsize_bf16_vs_oracle(full_ref):
     with torch.no_grad():
         ev = m(ref["x"].cuda())
     ee = rel_err(ev, f64["eval"])
-    print(f"bf16 HIP eval-mode logits rel-L2 {ee:.3e}; autocast eval {rel_err(ac['eval'], f64['eval']):.3e}")
+    print(f"{prec} HIP eval-mode logits rel-L2 {ee:.3e}; autocast eval {rel_err(ac['eval'], f64['eval']):.3e}")
     assert ee <= 1e-2, ee        # SURVEY §8(d)'s bf16 logits gate holds once BN uses running statistics

@@ -67,3 +67,19 @@ def test_confusion_ignore_index_and_out_of_range():
     assert np.array_equal(m.get_confusion_matrix(), ref.numpy())
     m.reset()
     assert m.compute()["mean_dice"] == 0.0
+
+
+def test_metrics_accept_host_tensors():
+    """update() with CPU tensors (what the reference's loop takes) counts on the GPU: same matrix as the
+    device inputs, accumulated into one device matrix."""
+    from unet.utils.metrics import SegmentationMetrics, compute_dice
+    O = _o()
+    gen = torch.Generator().manual_seed(13)
+    z = torch.randn(2, 2, 33, 47, generator=gen)
+    t = torch.randint(0, 2, (2, 33, 47), generator=gen)
+    m = SegmentationMetrics(num_classes=2)
+    m.update(z, t)
+    m.update(z.cuda(), t)
+    assert np.array_equal(m.get_confusion_matrix(), (O.confusion_matrix(z.argmax(1), t, 2) * 2).numpy())
+    assert m.compute() == O.segmentation_scores(m.get_confusion_matrix(), m.class_names)
+    assert torch.equal(compute_dice(z, t).cpu(), compute_dice(z.cuda(), t.cuda()).cpu())

@@ -10,7 +10,8 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-DT = {"fp32": torch.float32, "bf16": torch.bfloat16}
+DT = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
+TN = {"fp32": "fp32", "bf16": "bf16", "fp16": "fp16"}   # kernel-name spelling
 
 
 def _lib():
@@ -46,7 +47,7 @@ def _act_ref(y, ab, relu=True):
 
 def _conv(prec, srcs, N, H, W, cin, w, k, out_mode, **kw):
     L, R = _lib(), _rt()
-    P = R.BF16 if prec == "bf16" else R.FP32
+    P = R._PRECISIONS[prec]
     transpose = kw.pop("transpose", False)
     cout = w.shape[1] if transpose else w.shape[0]
     wp = R.pack_weight(w, P, transpose=transpose)
@@ -71,7 +72,7 @@ CONV_SHAPES = [  # (N, H, W, Cin, Cout) — tile configs: BN 32/64/128, TH 8/16,
 ]
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("shape", CONV_SHAPES)
 @pytest.mark.parametrize("k", [3, 1])
 def test_conv_fwd_act(prec, shape, k):
@@ -87,7 +88,7 @@ def test_conv_fwd_act(prec, shape, k):
     d = _conv(prec, [_act_src(y, ab)], N, H, W, cin, w, k, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
     x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2)
     ref = F.conv2d(x, w, padding=k // 2).permute(0, 2, 3, 1)
-    tol = 2e-2 if prec == "bf16" else 1e-4
+    tol = 2e-2 if prec != "fp32" else 1e-4
     assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max()), (out.float() - ref).abs().max()
     # BN partial sums ([2][Cout][rows], from the fp32 accumulators)
     rows = L.load().unet_conv_stats_rows(d)
@@ -98,7 +99,7 @@ def test_conv_fwd_act(prec, shape, k):
     assert ((sums[1] - (r * r).sum(0)).abs() <= 4 * tol * (r * r).sum(0) + 1e-3).all()
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("shape", [(2, 16, 16, 32, 64), (1, 21, 30, 64, 128), (2, 8, 8, 128, 64)])
 def test_conv_fwd_pool_and_up_concat(prec, shape):
     """down.0 (max-pool of ACT) and up.0 ([gated skip, pad(up(ACT))]) loaders."""
@@ -114,7 +115,7 @@ def test_conv_fwd_pool_and_up_concat(prec, shape):
     _conv(prec, [_act_src(ys, ab, kind=L.SRC_POOL_ACT)], N, H, W, cin, w, 3, L.OUT_Y, out=out.data_ptr())
     x = F.max_pool2d(_act_ref(ys, ab).permute(0, 3, 1, 2), 2)
     ref = F.conv2d(x.to(dt).float(), w, padding=1).permute(0, 2, 3, 1)
-    tol = 2e-2 if prec == "bf16" else 1e-4
+    tol = 2e-2 if prec != "fp32" else 1e-4
     assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max())
     # concat [skip * sigmoid(gate), pad(up(act(dec)))]
     cs = cin // 2
@@ -140,7 +141,7 @@ def test_conv_fwd_pool_and_up_concat(prec, shape):
     assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max())
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("shape", [(2, 16, 16, 64, 32), (1, 24, 40, 128, 64), (2, 18, 20, 64, 128)])
 def test_conv_dgrad_split_and_pool(prec, shape):
     L = _lib()
@@ -157,7 +158,7 @@ def test_conv_dgrad_split_and_pool(prec, shape):
     o2 = torch.empty(N, H, W, cin - split, device="cuda")
     _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
           split=split, accum=1, accum2=0)
-    tol = 2e-2 if prec == "bf16" else 1e-4
+    tol = 2e-2 if prec != "fp32" else 1e-4
     got = torch.cat([o1 - 1.0, o2], -1)
     assert (got - ref).abs().max() <= tol * (1 + ref.abs().max())
     # pool-bwd routing: gradient of maxpool(act(ys)) at the pooled resolution
@@ -171,14 +172,14 @@ def test_conv_dgrad_split_and_pool(prec, shape):
     assert (da.permute(0, 3, 1, 2) - a.grad).abs().max() <= tol * (1 + ref.abs().max())
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("shape", [(2, 16, 16, 64, 64), (1, 24, 40, 32, 128), (2, 40, 36, 128, 256),
                                    (4, 32, 32, 96, 64), (4, 128, 128, 64, 64)])   # last: >32 split-K slabs
 @pytest.mark.parametrize("k", [3, 1])
 @pytest.mark.parametrize("kind", ["act", "pool"])
 def test_conv_wgrad(prec, shape, k, kind):
     L, R = _lib(), _rt()
-    P = R.BF16 if prec == "bf16" else R.FP32
+    P = R._PRECISIONS[prec]
     N, H, W, cin, cout = shape
     dt = DT[prec]
     torch.manual_seed(3)
@@ -205,16 +206,16 @@ def test_conv_wgrad(prec, shape, k, kind):
     wd.workspace = ws.data_ptr()
     L.call("unet_conv_wgrad", wd, R.stream())
     torch.cuda.synchronize()
-    tol = 1e-3 if prec == "bf16" else 1e-4
+    tol = 1e-3 if prec != "fp32" else 1e-4
     assert (dw - ref).abs().max() <= tol * (1 + ref.abs().max()), float((dw - ref).abs().max())
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("shape", [(2, 1, 40, 36, 64), (1, 3, 33, 50, 16), (4, 1, 64, 64, 8)])
 def test_first_conv_nchw_input(prec, shape):
     """inc.0: the fp32 NCHW model input read directly (csrc/smallcin.hip), fwd + BN sums + wgrad."""
     L, R = _lib(), _rt()
-    P = R.BF16 if prec == "bf16" else R.FP32
+    P = R._PRECISIONS[prec]
     N, cin, H, W, cout = shape
     dt = DT[prec]
     torch.manual_seed(4)
@@ -232,9 +233,9 @@ def test_first_conv_nchw_input(prec, shape):
     d.weight, d.out_mode, d.out, d.stats = wp.data_ptr(), L.OUT_Y, out.data_ptr(), st.data_ptr()
     L.call("unet_conv", d, R.stream())
     torch.cuda.synchronize()
-    xr = x.to(dt).float() if prec == "bf16" else x
+    xr = x.to(dt).float() if prec != "fp32" else x
     ref = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)
-    tol = 1e-2 if prec == "bf16" else 1e-5
+    tol = 1e-2 if prec != "fp32" else 1e-5
     assert (out.float() - ref).abs().max() <= tol * (1 + ref.abs().max())
     assert torch.allclose(st[0].sum(1), ref.sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
     assert torch.allclose(st[1].sum(1), (ref * ref).sum((0, 1, 2)), rtol=1e-4, atol=1e-2)
@@ -255,14 +256,14 @@ def test_first_conv_nchw_input(prec, shape):
     del xr
 
 
-@pytest.mark.parametrize("prec", ["bf16", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("shape", [(2, 8, 8, 64, 32, 0, 0), (1, 12, 20, 128, 64, 1, 2), (2, 5, 7, 32, 16, 0, 1)])
 def test_conv_transpose_k2s2(prec, shape):
     """Up(bilinear=False): ConvTranspose2d(k=2, s=2, bias) as a 1x1 conv with the SHUFFLE2 epilogue,
     and its backward (space-to-depth prep + bias colsum + 1x1 wgrad + 1x1 dgrad), vs torch fp32."""
     from unet._hip.stages import ConvTStage, Grads
     R = _rt()
-    P = R.BF16 if prec == "bf16" else R.FP32
+    P = R._PRECISIONS[prec]
     N, h, w, cin, ct, pt, pl = shape
     dt = DT[prec]
     torch.manual_seed(5)
@@ -276,7 +277,7 @@ def test_conv_transpose_k2s2(prec, shape):
     u = st.forward(P, a)
     x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2).requires_grad_(True)
     ref = m(x)
-    tol = 2e-2 if prec == "bf16" else 1e-4
+    tol = 2e-2 if prec != "fp32" else 1e-4
     assert (u.data.float().permute(0, 3, 1, 2) - ref).abs().max() <= tol * (1 + ref.abs().max())
     # backward through a padded placement
     Hp, Wp = 2 * h + pt + 1, 2 * w + pl + 2
@@ -289,7 +290,7 @@ def test_conv_transpose_k2s2(prec, shape):
     ref.backward(g.permute(0, 3, 1, 2))
     gw, gb = grads[m.weight], grads[m.bias]
     assert gw.shape == m.weight.shape
-    tw = 1e-3 if prec == "bf16" else 1e-4
+    tw = 1e-3 if prec != "fp32" else 1e-4
     assert (gw - m.weight.grad).abs().max() <= tw * (1 + m.weight.grad.abs().max())
     assert (gb - m.bias.grad).abs().max() <= 1e-4 * (1 + m.bias.grad.abs().max())
     gx = x.grad.permute(0, 2, 3, 1)
@@ -494,10 +495,11 @@ Y_BENCH = [
 
 @pytest.mark.parametrize("shape", Y_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
 @pytest.mark.parametrize("stats", [True, False])
-def test_conv3_bench_tiles_y(shape, stats):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv3_bench_tiles_y(prec, shape, stats):
     L = _lib()
     N, H, W, cin, cout, want = shape
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(11)
     y = _rand(N, H, W, cin, dt=dt)
     ab = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2])
@@ -508,13 +510,13 @@ def test_conv3_bench_tiles_y(shape, stats):
     st = None
     if stats:
         d0 = L.ConvDesc()
-        d0.dtype, d0.N, d0.H, d0.W, d0.Cin, d0.Cout, d0.ksize, d0.nsrc = L.BF16, N, H, W, cin, cout, 3, 1
+        d0.dtype, d0.N, d0.H, d0.W, d0.Cin, d0.Cout, d0.ksize, d0.nsrc = _rt()._PRECISIONS[prec].code, N, H, W, cin, cout, 3, 1
         d0.src[0] = _act_src(y, ab)
         rows = L.load().unet_conv_stats_rows(d0)
         st = torch.empty(2, cout, rows, device="cuda")
         kw["stats"] = st.data_ptr()
-    d = _conv("bf16", [_act_src(y, ab)], N, H, W, cin, w, 3, L.OUT_Y, **kw)
-    assert _variant(d) == want, _variant(d)
+    d = _conv(prec, [_act_src(y, ab)], N, H, W, cin, w, 3, L.OUT_Y, **kw)
+    assert _variant(d) == want.replace("bf16", TN[prec]), _variant(d)
     assert _persistent(N, H, W, 8, cout, 64 if cout <= 64 else 128, True) > 1
     x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2)
     ref = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)
@@ -537,10 +539,11 @@ DGRAD_BENCH = [
 
 
 @pytest.mark.parametrize("shape", DGRAD_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
-def test_conv3_bench_tiles_dgrad_f32(shape):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv3_bench_tiles_dgrad_f32(prec, shape):
     L = _lib()
     N, H, W, cin, cout, want = shape
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(12)
     dy = _rand(N, H, W, cout, dt=dt)
     w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
@@ -550,9 +553,9 @@ def test_conv3_bench_tiles_dgrad_f32(shape):
     split = cin // 2
     o1 = torch.full((N, H, W, split), 0.5, device="cuda")
     o2 = torch.full((N, H, W, cin - split), float("nan"), device="cuda")
-    d = _conv("bf16", [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
+    d = _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
               split=split, accum=1, accum2=0)
-    assert _variant(d) == want, _variant(d)
+    assert _variant(d) == want.replace("bf16", TN[prec]), _variant(d)
     assert _persistent(N, H, W, 16, cin, 128 if cin > 64 else 64, False) > 1
     got = torch.cat([o1 - 0.5, o2], -1)
     _close_bf16(got, ref, "dgrad f32")
@@ -560,11 +563,12 @@ def test_conv3_bench_tiles_dgrad_f32(shape):
 
 @pytest.mark.parametrize("shape", [(4, 512, 512, 64, 64), (4, 256, 256, 128, 128), (3, 200, 328, 64, 64)],
                          ids=lambda s: "x".join(map(str, s)))
-def test_conv3_bench_tiles_dgrad_y(shape):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv3_bench_tiles_dgrad_y(prec, shape):
     """bf16 gradient of a DoubleConv's middle activation (the y epilogue without BN sums)."""
     L = _lib()
     N, H, W, cin, cout = shape
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(13)
     dy = _rand(N, H, W, cout, dt=dt)
     w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
@@ -572,8 +576,8 @@ def test_conv3_bench_tiles_dgrad_y(shape):
     src = L.Src()
     src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
     out = torch.empty(N, H, W, cin, dtype=dt, device="cuda")
-    d = _conv("bf16", [src], N, H, W, cout, w, 3, L.OUT_Y, transpose=True, out=out.data_ptr())
-    assert _variant(d).startswith("conv3_kernel<bf16,3,1,4,"), _variant(d)
+    d = _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_Y, transpose=True, out=out.data_ptr())
+    assert _variant(d).startswith(f"conv3_kernel<{TN[prec]},3,1,4,"), _variant(d)
     _close_bf16(out.float(), ref, "dgrad y")
 
 
@@ -587,10 +591,11 @@ POOL_BENCH = [
 
 @pytest.mark.parametrize("shape", POOL_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
 @pytest.mark.parametrize("with_code", [True, False])
-def test_conv3_bench_tiles_pool_bwd(shape, with_code):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv3_bench_tiles_pool_bwd(prec, shape, with_code):
     L, R = _lib(), _rt()
     N, H, W, cin, cout, want = shape
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(14)
     dy = _rand(N, H, W, cout, dt=dt)
     w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
@@ -602,14 +607,14 @@ def test_conv3_bench_tiles_pool_bwd(shape, with_code):
     if with_code:
         pooled = torch.empty(N, H, W, cin, dtype=dt, device="cuda")
         code = torch.empty(N, H, W, cin, dtype=torch.uint8, device="cuda")
-        L.call("unet_materialize_pool", L.BF16, psrc, N, H, W, pooled.data_ptr(), code.data_ptr(), R.stream())
+        L.call("unet_materialize_pool", _rt()._PRECISIONS[prec].code, psrc, N, H, W, pooled.data_ptr(), code.data_ptr(), R.stream())
         kw["pool_code"] = code.data_ptr()
     src = L.Src()
     src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
     da = torch.zeros(N, 2 * H, 2 * W, cin, device="cuda")
-    d = _conv("bf16", [src], N, H, W, cout, w, 3, L.OUT_POOL_BWD, transpose=True, out=da.data_ptr(),
+    d = _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_POOL_BWD, transpose=True, out=da.data_ptr(),
               pool_src=_act_src(ys, ab), **kw)
-    assert _variant(d) == want, _variant(d)
+    assert _variant(d) == want.replace("bf16", TN[prec]), _variant(d)
     a = _act_ref(ys, ab).permute(0, 3, 1, 2).requires_grad_(True)
     F.max_pool2d(a, 2).backward(ref.permute(0, 3, 1, 2))
     _close_bf16(da.permute(0, 3, 1, 2), a.grad, "pool bwd")
@@ -617,11 +622,12 @@ def test_conv3_bench_tiles_pool_bwd(shape, with_code):
 
 @pytest.mark.parametrize("shape", [(4, 512, 512, 64, 64), (4, 256, 256, 64, 128), (4, 64, 64, 512, 512)],
                          ids=lambda s: "x".join(map(str, s)))
-def test_wgrad_bench_sizes(shape):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_wgrad_bench_sizes(prec, shape):
     """3x3 weight gradients at the benchmark's sizes (wgrad2, split-K slabs + fixed-order reduction)."""
     L, R = _lib(), _rt()
     N, H, W, cin, cout = shape
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(15)
     dy = _rand(N, H, W, cout, dt=dt)
     ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
@@ -629,7 +635,7 @@ def test_wgrad_bench_sizes(shape):
     x = _act_ref(y, ab).to(dt).float().permute(0, 3, 1, 2)
     ref = torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), dy.float().permute(0, 3, 1, 2), padding=1)
     wd = L.WgradDesc()
-    wd.dtype = R.BF16.code
+    wd.dtype = _rt()._PRECISIONS[prec].code
     wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = N, H, W, cin, cout, 3, 1
     wd.src[0] = _act_src(y, ab)
     wd.dy = dy.data_ptr()
@@ -646,12 +652,13 @@ def test_wgrad_bench_sizes(shape):
 @pytest.mark.parametrize("shape", [(4, 128, 128, 64, 128), (2, 66, 70, 128, 64), (4, 256, 256, 128, 64)],
                          ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("kind", ["plain", "act", "gated+plain"])
-def test_wgrad_source_kinds(shape, kind):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_wgrad_source_kinds(prec, shape, kind):
     """wgrad2's compile-time source-kind staging (plain map / BN+ReLU source / the up-block concat of a
     gated skip and the stored upsampled map) vs torch's conv2d_weight on the same activation."""
     L, R = _lib(), _rt()
     N, H, W, cin, cout = shape
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(16)
     dy = _rand(N, H, W, cout, dt=dt)
     if kind == "plain":
@@ -679,7 +686,7 @@ def test_wgrad_source_kinds(shape, kind):
     ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2), (cout, cin, 3, 3), dy.float().permute(0, 3, 1, 2),
                                       padding=1)
     wd = L.WgradDesc()
-    wd.dtype = R.BF16.code
+    wd.dtype = _rt()._PRECISIONS[prec].code
     wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = N, H, W, cin, cout, 3, len(srcs)
     for i, s in enumerate(srcs):
         wd.src[i] = s

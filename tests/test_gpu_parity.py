@@ -83,9 +83,10 @@ def test_model_fp32_vs_golden(golden_models, name):
     assert max_abs(ev, rec["eval_logits"]) <= 1e-4 * (1 + float(rec["eval_logits"].abs().max()))
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("name", ["attention_unet_b8", "unet_b8"])
-def test_model_bf16_vs_golden(golden_models, name):
-    """bf16 operand mode: no worse than the reference's own network run under torch.autocast(bf16)
+def test_model_16bit_vs_golden(golden_models, name, prec):
+    """bf16 / fp16 operand mode: no worse than the reference's own network run under torch.autocast(same type)
     (the oracle's ATen ops on the GPU), measured against the same fp32 golden logits/loss.  On this
     tiny random-init net the inherent bf16 error is large (logits rel-L2 ~4-9 %), so a fixed
     tolerance would be meaningless; the bound is relative to PyTorch's own bf16 execution."""
@@ -96,17 +97,18 @@ def test_model_bf16_vs_golden(golden_models, name):
     from unet.utils.loss import DiceBCELoss
     rec = golden_models[name]
     m = build_model(rec)
-    m.hip_precision = "bf16"
+    m.hip_precision = prec
     out = m(rec["x"].cuda())
     loss = DiceBCELoss()(out, rec["t"].cuda())
     loss.backward()
     p = {k: v.cuda() for k, v in rec["init"].items()}
     fwd = O.unet_forward if rec["kind"] == "unet" else O.attention_unet_forward
-    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.no_grad(), torch.autocast("cuda", dtype={"bf16": torch.bfloat16, "fp16": torch.float16}[prec]):
         ac = fwd(p, rec["x"].cuda(), training=True).float()
     ac_loss = O.dice_bce_loss(ac, rec["t"].cuda())
     ref = rec["outputs"][0]
     e_ours, e_torch = rel_err(out, ref), rel_err(ac, ref)
+    print(f"\n{name} {prec}: logits rel-L2 HIP {e_ours:.3e}, autocast {e_torch:.3e}")
     assert e_ours <= 1.5 * e_torch + 1e-2, (e_ours, e_torch)
     l_ref = float(rec["loss"])
     assert abs(float(loss) - l_ref) <= 1.5 * abs(float(ac_loss) - l_ref) + 2e-3 * abs(l_ref)
@@ -168,3 +170,91 @@ def test_deep_supervision_fused_vs_oracle(golden_losses, base, K):
     assert abs(float(loss.detach()) - float(ref)) <= 1e-5 * (1 + abs(float(ref))), (float(loss), float(ref))
     for a, b in zip(zg, zr):
         assert max_abs(a.grad, b.grad) <= 1e-6 + 1e-4 * float(b.grad.abs().max())
+
+
+def test_fp16_grad_scaler_steps():
+    """fp16 operand mode under torch.amp.GradScaler (config C5's loss scaling): (1) an overflowing scale
+    (2^40: the fp16 activation gradients saturate) is detected — the step is skipped, the parameters stay
+    put and the scale backs off; (2) at a sane scale the unscaled gradients are no further from the
+    fp32-operand gradients than the reference network's own torch.autocast(fp16) gradients (same scale)
+    are from its fp32 ones (all-parameter rel-L2, 1.1x + 1e-2); (3) three scaled AdamW steps track the
+    fp32-operand run's losses within 2e-2."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from oracle import unet_oracle as O
+    from unet.models import AttentionUNet
+    from unet.utils.loss import DiceBCELoss
+    torch.manual_seed(3)
+    x = torch.rand(2, 3, 128, 128, device="cuda") * 2 - 1
+    t = torch.zeros(2, 128, 128, dtype=torch.int64, device="cuda")
+    t[0, 30:60, 40:90] = 1
+    t[1, 70:100, 10:50] = 1
+    crit = DiceBCELoss()
+
+    def make(prec):
+        torch.manual_seed(0)
+        m = AttentionUNet(3, 2, base_features=16).cuda().train()
+        m.hip_precision = prec
+        return m
+
+    m = make("fp16")
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    sc = torch.amp.GradScaler("cuda", init_scale=2.0 ** 40)
+    before = [p.detach().clone() for p in m.parameters()]
+    sc.scale(crit(m(x), t)).backward()
+    sc.step(opt)
+    sc.update()
+    assert sc.get_scale() < 2.0 ** 40
+    assert all(torch.equal(a, p.detach()) for a, p in zip(before, m.parameters()))
+
+    def rel_all(ga, gb):
+        num = sum(float((a - b).double().pow(2).sum()) for a, b in zip(ga, gb))
+        return (num / sum(float(b.double().pow(2).sum()) for b in gb)) ** 0.5
+
+    scale = 1024.0
+    m16, m32 = make("fp16"), make("fp32")
+    names = [k for k, _ in m32.named_parameters()]
+    init = {k: v.detach().clone() for k, v in m32.state_dict().items()}
+    sc = torch.amp.GradScaler("cuda", init_scale=scale)
+    sc.scale(crit(m16(x), t)).backward()
+    opt16 = torch.optim.AdamW(m16.parameters(), lr=1e-3)
+    sc.unscale_(opt16)
+    crit(m32(x), t).backward()
+    e_ours = rel_all([p.grad for p in m16.parameters()], [p.grad for p in m32.parameters()])
+
+    def oracle_grads(autocast):
+        p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v.clone())
+             for k, v in init.items()}
+        if autocast:
+            with torch.autocast("cuda", dtype=torch.float16):
+                z = O.attention_unet_forward(p, x, training=True)
+            (O.dice_bce_loss(z.float(), t) * scale).backward()
+            return [p[k].grad / scale for k in names]
+        O.dice_bce_loss(O.attention_unet_forward(p, x, training=True), t).backward()
+        return [p[k].grad for k in names]
+
+    e_torch = rel_all(oracle_grads(True), oracle_grads(False))
+    print(f"\nfp16 + GradScaler grads vs fp32 operands: HIP rel-L2 {e_ours:.3e}; autocast-fp16 {e_torch:.3e}")
+    assert e_ours <= 1.1 * e_torch + 1e-2, (e_ours, e_torch)
+    opt16.zero_grad()
+    m16, m32 = make("fp16"), make("fp32")
+    o16 = torch.optim.AdamW(m16.parameters(), lr=1e-3)
+    o32 = torch.optim.AdamW(m32.parameters(), lr=1e-3)
+    sc = torch.amp.GradScaler("cuda", init_scale=scale)
+    for _ in range(3):
+        l16 = crit(m16(x), t)
+        sc.scale(l16).backward()
+        sc.unscale_(o16)
+        torch.nn.utils.clip_grad_norm_(m16.parameters(), 1.0)
+        sc.step(o16)
+        sc.update()
+        o16.zero_grad()
+        l32 = crit(m32(x), t)
+        l32.backward()
+        torch.nn.utils.clip_grad_norm_(m32.parameters(), 1.0)
+        o32.step()
+        o32.zero_grad()
+        print(f"loss fp16 {float(l16):.5f} fp32 {float(l32):.5f}")
+        assert abs(float(l16) - float(l32)) <= 2e-2 * abs(float(l32)), (float(l16), float(l32))
+    assert sc.get_scale() == scale      # no overflow at a sane scale

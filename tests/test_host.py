@@ -2,6 +2,8 @@
 and the fail-loudly contract (no CPU fallback)."""
 
 import re
+
+import numpy as np
 from pathlib import Path
 
 import pytest
@@ -99,3 +101,27 @@ def test_product_never_imports_oracle():
     pkg = ROOT / "unet-segment-pytorch_amd"
     for f in pkg.rglob("*.py"):
         assert "oracle" not in f.read_text().replace("oracle/ is test", ""), f
+
+
+@pytest.mark.parametrize("K", [2, 3, 5])
+def test_metrics_compute_matches_reference_formulas(K):
+    """SegmentationMetrics.compute() (vectorised over classes) against the oracle's per-class restatement
+    of metrics.py:86-143 on random confusion matrices, incl. absent classes (zero row + column), a class
+    never predicted, and the empty matrix: identical floats."""
+    import torch
+    from oracle import unet_oracle as O
+    from unet.utils.metrics import SegmentationMetrics
+    rng = np.random.default_rng(K)
+    mats = [rng.integers(0, 10 ** rng.integers(1, 7), (K, K)) for _ in range(20)]
+    z = rng.integers(0, 1000, (K, K))
+    z[1, :] = 0
+    z[:, 1] = 0
+    mats.append(z)
+    z = rng.integers(0, 1000, (K, K))
+    z[:, 0] = 0
+    mats.append(z)
+    mats.append(np.zeros((K, K), np.int64))
+    for cm in mats:
+        m = SegmentationMetrics(num_classes=K)
+        m._cm = torch.from_numpy(cm.astype(np.int64))
+        assert m.compute() == O.segmentation_scores(cm.astype(np.int64), m.class_names)

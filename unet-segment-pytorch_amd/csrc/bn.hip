@@ -348,12 +348,18 @@ int unet_bn_bwd_reduce(int dtype, int da_dtype, long long P, int C, const void* 
                        const float* shift, int relu, const float* mean, const float* invstd, float* partial,
                        void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == UNET_F32 && da_dtype != UNET_F32) { set_error("unet_bn_bwd_reduce: bf16 gradient needs bf16 y"); return UNET_ERR_ARG; }
+  if (da_dtype != UNET_F32 && da_dtype != dtype) { set_error("unet_bn_bwd_reduce: a 16-bit gradient needs y of the same type"); return UNET_ERR_ARG; }
   if (bn_vec_ok(C)) {
     const int rows = reduce_rows_vec(P, C);
-    if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
+    if (dtype == UNET_F16 && da_dtype == UNET_F16)
+      hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<f16, f16>), dim3(rows), dim3(256), 0, st, P, C, (const f16*)da,
+                         (const f16*)y, scale, shift, relu, mean, invstd, partial, rows);
+    else if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
       hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<bf16, bf16>), dim3(rows), dim3(256), 0, st, P, C, (const bf16*)da,
                          (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
+    else if (dtype == UNET_F16)
+      hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<f16, float>), dim3(rows), dim3(256), 0, st, P, C, (const float*)da,
+                         (const f16*)y, scale, shift, relu, mean, invstd, partial, rows);
     else if (dtype == UNET_BF16)
       hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<bf16, float>), dim3(rows), dim3(256), 0, st, P, C, (const float*)da,
                          (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
@@ -364,9 +370,15 @@ int unet_bn_bwd_reduce(int dtype, int da_dtype, long long P, int C, const void* 
   }
   const int cl = chan_lanes(C), rows = reduce_rows(P, C);
   dim3 grid(cdiv(C, cl), rows);
-  if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
+  if (dtype == UNET_F16 && da_dtype == UNET_F16)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<f16, f16>), grid, dim3(256), 0, st, P, C, cl, (const f16*)da,
+                       (const f16*)y, scale, shift, relu, mean, invstd, partial, rows);
+  else if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, bf16>), grid, dim3(256), 0, st, P, C, cl, (const bf16*)da,
                        (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
+  else if (dtype == UNET_F16)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<f16, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
+                       (const f16*)y, scale, shift, relu, mean, invstd, partial, rows);
   else if (dtype == UNET_BF16)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<bf16, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
                        (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows);
@@ -387,13 +399,19 @@ int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int 
 int unet_bn_bwd_apply(int dtype, int da_dtype, long long P, int C, const void* da, const void* y, const float* scale,
                       const float* shift, int relu, const float* coef, void* dy, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == UNET_F32 && da_dtype != UNET_F32) { set_error("unet_bn_bwd_apply: bf16 gradient needs bf16 y"); return UNET_ERR_ARG; }
+  if (da_dtype != UNET_F32 && da_dtype != dtype) { set_error("unet_bn_bwd_apply: a 16-bit gradient needs y of the same type"); return UNET_ERR_ARG; }
   if (bn_vec_ok(C)) {
     long long b = (P * (C / 8) + 255) / 256;
     if (b > 8192) b = 8192;
-    if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
+    if (dtype == UNET_F16 && da_dtype == UNET_F16)
+      hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<f16, f16>), dim3((int)b), dim3(256), 0, st, P, C, (const f16*)da,
+                         (const f16*)y, scale, shift, relu, coef, (f16*)dy);
+    else if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
       hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<bf16, bf16>), dim3((int)b), dim3(256), 0, st, P, C, (const bf16*)da,
                          (const bf16*)y, scale, shift, relu, coef, (bf16*)dy);
+    else if (dtype == UNET_F16)
+      hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<f16, float>), dim3((int)b), dim3(256), 0, st, P, C, (const float*)da,
+                         (const f16*)y, scale, shift, relu, coef, (f16*)dy);
     else if (dtype == UNET_BF16)
       hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<bf16, float>), dim3((int)b), dim3(256), 0, st, P, C, (const float*)da,
                          (const bf16*)y, scale, shift, relu, coef, (bf16*)dy);
@@ -404,9 +422,15 @@ int unet_bn_bwd_apply(int dtype, int da_dtype, long long P, int C, const void* d
   }
   const int cl = chan_lanes(C), rows = reduce_rows(P, C);
   dim3 grid(cdiv(C, cl), rows);
-  if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
+  if (dtype == UNET_F16 && da_dtype == UNET_F16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<f16, f16>), grid, dim3(256), 0, st, P, C, cl, (const f16*)da,
+                       (const f16*)y, scale, shift, relu, coef, (f16*)dy, rows);
+  else if (dtype == UNET_BF16 && da_dtype == UNET_BF16)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, bf16>), grid, dim3(256), 0, st, P, C, cl, (const bf16*)da,
                        (const bf16*)y, scale, shift, relu, coef, (bf16*)dy, rows);
+  else if (dtype == UNET_F16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<f16, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
+                       (const f16*)y, scale, shift, relu, coef, (f16*)dy, rows);
   else if (dtype == UNET_BF16)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
                        (const bf16*)y, scale, shift, relu, coef, (bf16*)dy, rows);

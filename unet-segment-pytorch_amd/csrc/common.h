@@ -7,8 +7,10 @@
 namespace unet {
 
 typedef __bf16 bf16;
+typedef _Float16 f16;   // fp16 operand mode (BASELINE C5): same 16-bit storage and MFMA rate as bf16
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(4))) short i16x4;
 
 constexpr int WAVE = 64;
@@ -25,12 +27,18 @@ template <> struct Vec<bf16> {
   static constexpr int N = 8;
   typedef uint4 type;
 };
+template <> struct Vec<f16> {
+  static constexpr int N = 8;
+  typedef uint4 type;
+};
 
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+__device__ __forceinline__ float to_f(f16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f(float x);
 template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+template <> __device__ __forceinline__ f16 from_f<f16>(float x) { return (f16)x; }
 
 // load VEC elements (16 B aligned) into floats
 template <typename T> __device__ __forceinline__ void load_vec(const T* p, float* v);
@@ -47,9 +55,20 @@ template <> __device__ __forceinline__ void load_vec<bf16>(const bf16* p, float*
     v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
   }
 }
+template <> __device__ __forceinline__ void load_vec<f16>(const f16* p, float* v) {
+  const f16x8 q = *reinterpret_cast<const f16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)q[i];
+}
 template <typename T> __device__ __forceinline__ void store_vec(T* p, const float* v);
 template <> __device__ __forceinline__ void store_vec<float>(float* p, const float* v) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> __device__ __forceinline__ void store_vec<f16>(f16* p, const float* v) {
+  f16x8 q;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = (f16)v[i];
+  *reinterpret_cast<f16x8*>(p) = q;
 }
 template <> __device__ __forceinline__ void store_vec<bf16>(bf16* p, const float* v) {
   bf16 b[8];
@@ -76,5 +95,58 @@ void set_error(const char* msg);
 int check_launch(const char* what);
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// 16-byte vector of 8 x 16-bit values <-> 8 floats, for either 16-bit operand type
+template <typename T>
+__device__ __forceinline__ void unpack8_16(const uint4& q, float* v) {
+  if constexpr (__is_same(T, bf16)) {
+    const unsigned u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  } else {
+    const f16x8 h = __builtin_bit_cast(f16x8, q);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)h[i];
+  }
+}
+template <typename T>
+__device__ __forceinline__ uint4 pack8_16(const float* v) {
+  if constexpr (__is_same(T, bf16)) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    unsigned u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16x2 p = {(__bf16)v[2 * i], (__bf16)v[2 * i + 1]};
+      u[i] = __builtin_bit_cast(unsigned, p);
+    }
+    return make_uint4(u[0], u[1], u[2], u[3]);
+  } else {
+    f16x8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (f16)v[i];
+    return __builtin_bit_cast(uint4, h);
+  }
+}
+template <typename T>
+__device__ __forceinline__ unsigned pack2_16(float a, float b) {
+  if constexpr (__is_same(T, bf16)) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    const bf16x2 p = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(unsigned, p);
+  } else {
+    typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+    const f16x2 p = {(f16)a, (f16)b};
+    return __builtin_bit_cast(unsigned, p);
+  }
+}
+
+// run `body` with T = float / bf16 / f16 for a UNET_F32 / UNET_BF16 / UNET_F16 code
+#define UNET_DISPATCH_T(code, ...)                                  \
+  ((code) == UNET_BF16 ? [&]() { using T = bf16; return __VA_ARGS__; }()  \
+   : (code) == UNET_F16 ? [&]() { using T = f16; return __VA_ARGS__; }()  \
+                        : [&]() { using T = float; return __VA_ARGS__; }())
 
 }  // namespace unet

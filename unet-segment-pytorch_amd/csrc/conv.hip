@@ -367,7 +367,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv2_kernel(const unet_conv_des
         for (int j = 0; j < NTN; ++j) {
           typename M::frag b;
           const uint4 q = B[t & 1][j];
-          if constexpr (sizeof(T) == 2) b = __builtin_bit_cast(bf16x8, q);
+          if constexpr (sizeof(T) == 2) b = __builtin_bit_cast(typename M::frag, q);
           else b = __uint_as_float(ks == 0 ? q.x : ks == 1 ? q.y : ks == 2 ? q.z : q.w);
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc[i][j] = M::mma(a[i], b, acc[i][j]);
@@ -440,7 +440,7 @@ static ConvCfg pick_cfg(const unet_conv_desc* d) {
   // under the other's MFMAs
   // (measured: faster for the y epilogue; the fp32 dgrad and pool-routing epilogues spill in the 4-wave
   // tile and keep the 16-row one)
-  const bool w4 = conv3_w4_enabled() && d->dtype == UNET_BF16 && d->ksize == 3 && c.raw == 1 &&
+  const bool w4 = conv3_w4_enabled() && d->dtype != UNET_F32 && d->ksize == 3 && c.raw == 1 &&
                   d->out_mode == UNET_OUT_Y;
   if (d->Cout <= 32) {
     c.wm = 2; c.wn = 2; c.ntn = 1;
@@ -494,8 +494,8 @@ int smallcin_conv(const unet_conv_desc* d, hipStream_t st);
 // the pipelined kernel needs every source channel vector to be one aligned 16-byte load, and every
 // source tensor addressable with 32-bit byte offsets
 static bool fast_eligible(const unet_conv_desc* d) {
-  const int vec = d->dtype == UNET_BF16 ? 8 : 4;
-  const int es = d->dtype == UNET_BF16 ? 2 : 4;
+  const int vec = d->dtype != UNET_F32 ? 8 : 4;
+  const int es = d->dtype != UNET_F32 ? 2 : 4;
   for (int i = 0; i < d->nsrc; ++i) {
     const unet_src& s = d->src[i];
     if (s.kind == UNET_SRC_NCHW_F32 || s.C % vec) return false;
@@ -508,7 +508,9 @@ template <typename T>
 static int dispatch_conv(const unet_conv_desc* d, hipStream_t st) {
   if (!fast_eligible(d)) return dispatch_generic<T>(d, st);
   const ConvCfg c = pick_cfg(d);
-  if (conv3_eligible(d)) return dispatch_conv3(d, c, st);
+  if constexpr (sizeof(T) == 2) {
+    if (conv3_eligible(d)) return dispatch_conv3<T>(d, c, st);
+  }
   if (d->ksize == 3) return c.raw == 4 ? dispatch_cfg<T, 3, 4>(d, c, st) : dispatch_cfg<T, 3, 1>(d, c, st);
   return c.raw == 4 ? dispatch_cfg<T, 1, 4>(d, c, st) : dispatch_cfg<T, 1, 1>(d, c, st);
 }
@@ -594,6 +596,8 @@ using namespace unet;
 
 extern "C" {
 
+static const char* tname(int dtype) { return dtype == UNET_BF16 ? "bf16" : dtype == UNET_F16 ? "fp16" : "fp32"; }
+
 int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8); }
 
 int unet_conv_stats_rows(const unet_conv_desc* d) {
@@ -606,12 +610,12 @@ int unet_conv_stats_rows(const unet_conv_desc* d) {
 
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
   if (smallcin_conv_ok(d)) {
-    snprintf(buf, len, "smallcin_fwd_kernel<%s>", d->dtype == UNET_BF16 ? "bf16" : "fp32");
+    snprintf(buf, len, "smallcin_fwd_kernel<%s>", tname(d->dtype));
     return 0;
   }
   if (pw_conv_ok(d)) return pw_conv_variant(d, buf, len);
   if (!fast_eligible(d)) {
-    snprintf(buf, len, "conv_generic_kernel<%s,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize,
+    snprintf(buf, len, "conv_generic_kernel<%s,%d,%d>", tname(d->dtype), d->ksize,
              d->Cout <= 32 ? 32 : 64);
     return 0;
   }
@@ -619,15 +623,15 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
   if (conv3_eligible(d)) {
     // the (wm, wn, ntn) block tile of pick_cfg; 16-row tiles run as MI=8 waves (dispatch_conv3)
     if (c.w4) {
-      snprintf(buf, len, "conv3_kernel<bf16,3,1,4,%d,8,1>", c.ntn / 2);
+      snprintf(buf, len, "conv3_kernel<%s,3,1,4,%d,8,1>", tname(d->dtype), c.ntn / 2);
       return 0;
     }
     const bool mi8 = c.raw == 1 && c.wm == 4 && (c.ntn == 4 || c.ntn == 2);
-    snprintf(buf, len, "conv3_kernel<bf16,3,%d,%d,%d,%d,%d>", mi8 ? 2 : c.wm, mi8 ? 4 : c.wn, mi8 ? c.ntn / 2 : c.ntn,
+    snprintf(buf, len, "conv3_kernel<%s,3,%d,%d,%d,%d,%d>", tname(d->dtype), mi8 ? 2 : c.wm, mi8 ? 4 : c.wn, mi8 ? c.ntn / 2 : c.ntn,
              mi8 ? 8 : 4, c.raw);
     return 0;
   }
-  snprintf(buf, len, "conv2_kernel<%s,%d,%d,%d,%d,%d>", d->dtype == UNET_BF16 ? "bf16" : "fp32", d->ksize, c.wm, c.wn,
+  snprintf(buf, len, "conv2_kernel<%s,%d,%d,%d,%d,%d>", tname(d->dtype), d->ksize, c.wm, c.wn,
            c.ntn, c.raw);
   return 0;
 }
@@ -653,7 +657,9 @@ int unet_pack_weights(int dtype, int count, const unet_pack_job* jobs, void* str
   int blocks = (int)((maxe + 255) / 256);
   if (blocks > 1024) blocks = 1024;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(pack_many_kernel<f16>, dim3(blocks, count), dim3(256), 0, st, pj);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(pack_many_kernel<bf16>, dim3(blocks, count), dim3(256), 0, st, pj);
   else
     hipLaunchKernelGGL(pack_many_kernel<float>, dim3(blocks, count), dim3(256), 0, st, pj);
@@ -661,7 +667,7 @@ int unet_pack_weights(int dtype, int count, const unet_pack_job* jobs, void* str
 }
 
 int unet_packed_weight_elems(int dtype, int Cout, int Cin, int ksize, int transpose) {
-  const int kc = dtype == UNET_BF16 ? 32 : 16;
+  const int kc = dtype != UNET_F32 ? 32 : 16;
   const int cols = transpose ? Cout : Cin;
   return packed_rows(Cout, Cin, transpose) * ksize * ksize * round_up(cols, kc);
 }
@@ -669,13 +675,16 @@ int unet_packed_weight_elems(int dtype, int Cout, int Cin, int ksize, int transp
 int unet_pack_weight(int dtype, const float* w, void* packed, int Cout, int Cin, int ksize, int transpose,
                      void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const int kc = dtype == UNET_BF16 ? 32 : 16;
+  const int kc = dtype != UNET_F32 ? 32 : 16;
   const int rows_pad = packed_rows(Cout, Cin, transpose);
   const int nchunks = cdiv(transpose ? Cout : Cin, kc);
   const long long total = (long long)rows_pad * nchunks * kc * ksize * ksize;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(pack_kernel<f16>, dim3(blocks), dim3(256), 0, st, w, (f16*)packed, Cout, Cin, ksize,
+                       transpose, rows_pad, nchunks);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(pack_kernel<bf16>, dim3(blocks), dim3(256), 0, st, w, (bf16*)packed, Cout, Cin, ksize,
                        transpose, rows_pad, nchunks);
   else
@@ -722,6 +731,7 @@ int unet_conv(const unet_conv_desc* d, void* stream) {
   if (smallcin_conv_ok(d)) return smallcin_conv(d, st);
   if (pw_conv_ok(d)) return pw_conv(d, st);
   if (d->dtype == UNET_BF16) return dispatch_conv<bf16>(d, st);
+  if (d->dtype == UNET_F16) return dispatch_conv<f16>(d, st);
   if (d->dtype == UNET_F32) return dispatch_conv<float>(d, st);
   set_error("unet_conv: bad dtype");
   return UNET_ERR_ARG;

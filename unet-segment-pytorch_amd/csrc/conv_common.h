@@ -15,6 +15,16 @@ template <> struct Mma<bf16> {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
 };
+template <> struct Mma<f16> {
+  static constexpr int KC = 32;
+  static constexpr int KSTEP = 32;
+  static constexpr int E = 8;
+  typedef f16x8 frag;
+  __device__ static __forceinline__ frag load(const f16* p) { return *reinterpret_cast<const f16x8*>(p); }
+  __device__ static __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
 template <> struct Mma<float> {
   static constexpr int KC = 16;
   static constexpr int KSTEP = 4;

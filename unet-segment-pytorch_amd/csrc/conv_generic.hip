@@ -230,6 +230,7 @@ int dispatch_generic(const unet_conv_desc* d, hipStream_t st) {
 }
 
 template int dispatch_generic<bf16>(const unet_conv_desc*, hipStream_t);
+template int dispatch_generic<f16>(const unet_conv_desc*, hipStream_t);
 template int dispatch_generic<float>(const unet_conv_desc*, hipStream_t);
 
 }  // namespace unet

@@ -117,7 +117,7 @@ __device__ __forceinline__ float group_sum(float v, int G) {
 template <typename T>
 __device__ __forceinline__ void load8(const T* p, float* v) {
   if constexpr (sizeof(T) == 2) {
-    load_vec<bf16>((const bf16*)p, v);
+    load_vec<T>(p, v);
   } else {
     load_vec<float>((const float*)p, v);
     load_vec<float>((const float*)p + 4, v + 4);
@@ -324,7 +324,10 @@ int unet_gate_psi(int dtype, long long P, int Ci, const void* gw, const void* xw
   const int rows = pix_rows(P);
   const int G = vec_group(Ci);
   if (G) {
-    if (dtype == UNET_BF16)
+    if (dtype == UNET_F16)
+      hipLaunchKernelGGL(psi_vec_kernel<f16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, G,
+                         (const f16*)gw, (const f16*)xw, gab, xab, wpsi, p, partial, rows);
+    else if (dtype == UNET_BF16)
       hipLaunchKernelGGL(psi_vec_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, G,
                          (const bf16*)gw, (const bf16*)xw, gab, xab, wpsi, p, partial, rows);
     else
@@ -332,7 +335,10 @@ int unet_gate_psi(int dtype, long long P, int Ci, const void* gw, const void* xw
                          (const float*)gw, (const float*)xw, gab, xab, wpsi, p, partial, rows);
     return check_launch("gate_psi");
   }
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(psi_kernel<f16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, (const f16*)gw,
+                       (const f16*)xw, gab, xab, wpsi, p, partial, rows);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(psi_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, (const bf16*)gw,
                        (const bf16*)xw, gab, xab, wpsi, p, partial, rows);
   else
@@ -347,7 +353,11 @@ int unet_gate_bwd1(int dtype, long long P, int Cx, const float* dxs, const void*
   const int rows = pix_rows(P);
   const int G = vec_group(Cx);
   if (G) {
-    if (dtype == UNET_BF16)
+    if (dtype == UNET_F16)
+      hipLaunchKernelGGL(gate_bwd1_vec_kernel<f16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, G, dxs,
+                         (const f16*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial,
+                         rows);
+    else if (dtype == UNET_BF16)
       hipLaunchKernelGGL(gate_bwd1_vec_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, G, dxs,
                          (const bf16*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial,
                          rows);
@@ -357,7 +367,10 @@ int unet_gate_bwd1(int dtype, long long P, int Cx, const float* dxs, const void*
                          rows);
     return check_launch("gate_bwd1");
   }
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(gate_bwd1_kernel<f16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, dxs,
+                       (const f16*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial, rows);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(gate_bwd1_kernel<bf16>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Cx, dxs,
                        (const bf16*)yx, sx, bx, relu, p, psi_ab, psi_mean, psi_invstd, dx, dx_accum, dq, partial, rows);
   else
@@ -374,7 +387,11 @@ int unet_gate_bwd2(int dtype, long long P, int Ci, const void* gw, const void* x
                    void* stream) {
   const int cl = chan_lanes_g(Ci), rows = rows_for(P, Ci);
   dim3 grid(cdiv(Ci, cl), rows);
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(gate_bwd2_kernel<f16>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const f16*)gw,
+                       (const f16*)xw, gab, xab, g_mean, g_invstd, x_mean, x_invstd, wpsi, dq, p, psi_coef, partial,
+                       rows);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(gate_bwd2_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const bf16*)gw,
                        (const bf16*)xw, gab, xab, g_mean, g_invstd, x_mean, x_invstd, wpsi, dq, p, psi_coef, partial,
                        rows);
@@ -390,7 +407,10 @@ int unet_gate_bwd3(int dtype, long long P, int Ci, const void* gw, const void* x
                    const float* xcoef, void* dgw, void* dxw, void* stream) {
   const int cl = chan_lanes_g(Ci), rows = rows_for(P, Ci);
   dim3 grid(cdiv(Ci, cl), rows);
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(gate_bwd3_kernel<f16>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const f16*)gw,
+                       (const f16*)xw, gab, xab, wpsi, dq, p, psi_coef, gcoef, xcoef, (f16*)dgw, (f16*)dxw, rows);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(gate_bwd3_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const bf16*)gw,
                        (const bf16*)xw, gab, xab, wpsi, dq, p, psi_coef, gcoef, xcoef, (bf16*)dgw, (bf16*)dxw, rows);
   else

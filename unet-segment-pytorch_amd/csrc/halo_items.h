@@ -18,12 +18,7 @@ namespace unet {
 template <typename T>
 __device__ __forceinline__ void unpack16(const uint4& q, float* v) {
   if constexpr (sizeof(T) == 2) {
-    const unsigned u[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] = __uint_as_float(u[i] << 16);
-      v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
-    }
+    unpack8_16<T>(q, v);
   } else {
     v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
   }

@@ -244,7 +244,7 @@ __global__ void outconv_fwd_vec_kernel(long long P, int HW, int C, int G, const 
   for (long long q = ((long long)blockIdx.x * nw + wave) * ppw + lane / G; q < P; q += stride) {
     float a[8];
     if constexpr (sizeof(T) == 2) {
-      load_vec<bf16>((const bf16*)y + q * C + c0, a);
+      load_vec<T>(y + q * C + c0, a);
     } else {
       load_vec<float>((const float*)y + q * C + c0, a);
       load_vec<float>((const float*)y + q * C + c0 + 4, a + 4);
@@ -342,8 +342,8 @@ __global__ void outconv_bwd_kernel(long long P, int HW, int C, int CL, int K, co
 // pixel per iteration — one 16-byte y load, two 16-byte da stores (or read-modify-writes); the K class
 // gradients of the pixel are loaded once per thread.  Same partial-sum table as outconv_bwd_kernel:
 // part[block][k][c] = Σ dl·a, part[block][K][k] = Σ dl (db).
-template <int KK>
-__global__ __launch_bounds__(256) void outconv_bwd_vec_kernel(long long P, int HW, int C, int G, const bf16* y,
+template <typename T, int KK>
+__global__ __launch_bounds__(256) void outconv_bwd_vec_kernel(long long P, int HW, int C, int G, const T* y,
                                                               const float* sc, const float* sf, int relu,
                                                               const float* w, const float* dl, float* da, int accum,
                                                               float* part) {
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) void outconv_bwd_vec_kernel(long long P, int H
 #pragma unroll
     for (int k = 0; k < KK; ++k) { dlk[k] = dl[(n * KK + k) * HW + hw]; db[k] += dlk[k]; }
     float a[8];
-    load_vec<bf16>(y + q * C + c0, a);
+    load_vec<T>(y + q * C + c0, a);
     float g[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -707,7 +707,10 @@ int unet_outconv_fwd(int dtype, long long N, int H, int W, int C, int K, const v
   if (G && K == 2) {
     long long blocks = (P * G + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    if (dtype == UNET_BF16)
+    if (dtype == UNET_F16)
+      hipLaunchKernelGGL((outconv_fwd_vec_kernel<f16, 2>), dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, P,
+                         H * W, C, G, (const f16*)y, scale, shift, relu, w, b, logits);
+    else if (dtype == UNET_BF16)
       hipLaunchKernelGGL((outconv_fwd_vec_kernel<bf16, 2>), dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, P,
                          H * W, C, G, (const bf16*)y, scale, shift, relu, w, b, logits);
     else
@@ -716,7 +719,10 @@ int unet_outconv_fwd(int dtype, long long N, int H, int W, int C, int K, const v
     return check_launch("outconv_fwd");
   }
   const size_t shm = (size_t)(K * C + 2 * C) * sizeof(float);
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(outconv_fwd_kernel<f16>, dim3(grid_for(P)), dim3(256), shm, (hipStream_t)stream, P, H * W, C, K,
+                       (const f16*)y, scale, shift, relu, w, b, logits);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(outconv_fwd_kernel<bf16>, dim3(grid_for(P)), dim3(256), shm, (hipStream_t)stream, P, H * W, C, K,
                        (const bf16*)y, scale, shift, relu, w, b, logits);
   else
@@ -732,13 +738,20 @@ int unet_outconv_bwd(int dtype, long long N, int H, int W, int C, int K, const v
   const long long P = N * H * (long long)W;
   const int cl = chan_lanes_m(C), rows = oc_rows(P);
   const int G = (C % 8 == 0 && C / 8 <= 256 && ((C / 8) & (C / 8 - 1)) == 0) ? C / 8 : 0;
-  if (dtype == UNET_BF16 && G && K == 2) {
-    hipLaunchKernelGGL(outconv_bwd_vec_kernel<2>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, H * W, C, G,
-                       (const bf16*)y, scale, shift, relu, w, dl, da, accum, partial);
+  if (dtype != UNET_F32 && G && K == 2) {
+    if (dtype == UNET_F16)
+      hipLaunchKernelGGL((outconv_bwd_vec_kernel<f16, 2>), dim3(rows), dim3(256), 0, (hipStream_t)stream, P, H * W, C, G,
+                         (const f16*)y, scale, shift, relu, w, dl, da, accum, partial);
+    else
+      hipLaunchKernelGGL((outconv_bwd_vec_kernel<bf16, 2>), dim3(rows), dim3(256), 0, (hipStream_t)stream, P, H * W, C, G,
+                         (const bf16*)y, scale, shift, relu, w, dl, da, accum, partial);
     return check_launch("outconv_bwd");
   }
   dim3 grid(cdiv(C, cl), rows);
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(outconv_bwd_kernel<f16>, grid, dim3(256), 0, (hipStream_t)stream, P, H * W, C, cl, K,
+                       (const f16*)y, scale, shift, relu, w, dl, da, accum, partial, rows);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(outconv_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, P, H * W, C, cl, K,
                        (const bf16*)y, scale, shift, relu, w, dl, da, accum, partial, rows);
   else
@@ -757,7 +770,10 @@ int unet_outconv_bwd_finalize(const float* partial, int rows, int C, int K, floa
 
 int unet_nchw_to_nhwc(int dtype, long long N, int C, int H, int W, const float* x, void* y, void* stream) {
   const long long total = N * C * (long long)H * W;
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<f16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H, W,
+                       x, (f16*)y);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H, W,
                        x, (bf16*)y);
   else
@@ -769,7 +785,10 @@ int unet_nchw_to_nhwc(int dtype, long long N, int C, int H, int W, const float* 
 int unet_nhwc_to_nchw(int dtype, long long N, int C, int H, int W, const void* x, const float* scale,
                       const float* shift, int relu, float* y, void* stream) {
   const long long total = N * C * (long long)H * W;
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<f16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H, W,
+                       (const f16*)x, scale, shift, relu, y);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H, W,
                        (const bf16*)x, scale, shift, relu, y);
   else
@@ -781,7 +800,10 @@ int unet_nhwc_to_nchw(int dtype, long long N, int C, int H, int W, const void* x
 int unet_gated_to_nchw(int dtype, long long N, int C, int H, int W, const void* x, const float* scale,
                        const float* shift, int relu, const float* p, const float* psi_ab, float* y, void* stream) {
   const long long total = N * C * (long long)H * W;
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(gated_to_nchw_kernel<f16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H,
+                       W, (const f16*)x, scale, shift, relu, p, psi_ab, y);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(gated_to_nchw_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, N, C, H,
                        W, (const bf16*)x, scale, shift, relu, p, psi_ab, y);
   else
@@ -801,7 +823,10 @@ int unet_convt_bwd_prep(int dtype, long long N, int h, int w, int Ct, int Hp, in
   }
   const int rows = oc_rows(N * h * w);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(convt_bwd_prep_kernel<f16>, dim3(rows), dim3(256), 0, st, N, h, w, Ct, Hp, Wp, pad_t, pad_l,
+                       d_up, (f16*)dy_s2d, partial, rows);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(convt_bwd_prep_kernel<bf16>, dim3(rows), dim3(256), 0, st, N, h, w, Ct, Hp, Wp, pad_t, pad_l,
                        d_up, (bf16*)dy_s2d, partial, rows);
   else
@@ -815,13 +840,13 @@ int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, 
     set_error("unet_materialize: bad arguments");
     return UNET_ERR_ARG;
   }
-  const int vec = dtype == UNET_BF16 ? 8 : 4;
+  const int vec = dtype != UNET_F32 ? 8 : 4;
   const long long total = N * H * (long long)W * ((src->C + vec - 1) / vec);
   long long b = (total + 255) / 256;
   if (b > 16384) b = 16384;
   const int cv = src->C / vec;
   // 32-bit gather offsets in item_issue: the source must stay below 4 GiB
-  const double bytes = (double)N * src->H * src->W * src->C * (dtype == UNET_BF16 ? 2 : 4);
+  const double bytes = (double)N * src->H * src->W * src->C * (dtype != UNET_F32 ? 2 : 4);
   if (src->C % vec == 0 && cv <= 256 && (cv & (cv - 1)) == 0 && bytes < 4294967296.0) {
     MatDesc md;
     md.nsrc = 1;
@@ -833,13 +858,19 @@ int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, 
     if (dtype == UNET_BF16) {
       if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<bf16, 4>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (bf16*)out);
       else hipLaunchKernelGGL((materialize_fast_kernel<bf16, 1>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (bf16*)out);
+    } else if (dtype == UNET_F16) {
+      if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<f16, 4>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (f16*)out);
+      else hipLaunchKernelGGL((materialize_fast_kernel<f16, 1>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (f16*)out);
     } else {
       if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<float, 4>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (float*)out);
       else hipLaunchKernelGGL((materialize_fast_kernel<float, 1>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (float*)out);
     }
     return check_launch("materialize");
   }
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(materialize_kernel<f16>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, *src, N, H, W,
+                       (f16*)out);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(materialize_kernel<bf16>, dim3((int)b), dim3(256), 0, (hipStream_t)stream, *src, N, H, W,
                        (bf16*)out);
   else
@@ -850,7 +881,7 @@ int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, 
 
 int unet_materialize_pool(int dtype, const unet_src* src, long long N, int H, int W, void* out, uint8_t* code,
                           void* stream) {
-  const int vec = dtype == UNET_BF16 ? 8 : 4;
+  const int vec = dtype != UNET_F32 ? 8 : 4;
   const int cv = src ? src->C / vec : 0;
   if (!src || !out || !code || src->kind != UNET_SRC_POOL_ACT || !src->scale || !src->shift || src->C % vec ||
       cv > 256 || (cv & (cv - 1)) || src->H < 2 * H || src->W < 2 * W) {
@@ -861,7 +892,9 @@ int unet_materialize_pool(int dtype, const unet_src* src, long long N, int H, in
   long long b = (total + 255) / 256;
   if (b > 16384) b = 16384;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == UNET_BF16)
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL(materialize_pool_kernel<f16>, dim3((int)b), dim3(256), 0, st, *src, N, H, W, (f16*)out, code);
+  else if (dtype == UNET_BF16)
     hipLaunchKernelGGL(materialize_pool_kernel<bf16>, dim3((int)b), dim3(256), 0, st, *src, N, H, W, (bf16*)out, code);
   else
     hipLaunchKernelGGL(materialize_pool_kernel<float>, dim3((int)b), dim3(256), 0, st, *src, N, H, W, (float*)out, code);

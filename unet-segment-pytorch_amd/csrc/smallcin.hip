@@ -300,6 +300,8 @@ int smallcin_conv(const unet_conv_desc* d, hipStream_t st) {
   const int rows = smallcin_rows((long long)d->N * d->H * d->W);
   if (d->dtype == UNET_BF16)
     hipLaunchKernelGGL(smallcin_fwd_kernel<bf16>, dim3(rows), dim3(256), 0, st, *d, rows);
+  else if (d->dtype == UNET_F16)
+    hipLaunchKernelGGL(smallcin_fwd_kernel<f16>, dim3(rows), dim3(256), 0, st, *d, rows);
   else
     hipLaunchKernelGGL(smallcin_fwd_kernel<float>, dim3(rows), dim3(256), 0, st, *d, rows);
   return check_launch("smallcin_fwd");
@@ -314,6 +316,8 @@ int smallcin_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
   float* part = (float*)d->workspace;
   if (d->dtype == UNET_BF16)
     hipLaunchKernelGGL(smallcin_wgrad_kernel<bf16>, dim3(rows), dim3(256), 0, st, *d, rows, part);
+  else if (d->dtype == UNET_F16)
+    hipLaunchKernelGGL(smallcin_wgrad_kernel<f16>, dim3(rows), dim3(256), 0, st, *d, rows, part);
   else
     hipLaunchKernelGGL(smallcin_wgrad_kernel<float>, dim3(rows), dim3(256), 0, st, *d, rows, part);
   int e = check_launch("smallcin_wgrad");

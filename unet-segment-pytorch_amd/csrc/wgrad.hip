@@ -18,18 +18,17 @@ constexpr int TH = 8, TW = 16, BM = TH * TW, NTHR = 256;
 // ------------------------------------------------------------------------------------------------
 constexpr int WG_BCO = 64;
 
-template <typename T> struct WgFrag;
-template <> struct WgFrag<bf16> {
+template <typename T> struct WgFrag {
   // A/B operand with K on the LDS ROW axis (pixels) and M/N on the column axis (channels):
   // two ds_read_b64_tr_b16 per operand (CDNA4 hardware transpose read).
   static constexpr int KSTEP = 32;
-  typedef bf16x8 frag;
-  __device__ static __forceinline__ frag tr_load(const bf16* row_q, const bf16* row_q4) {
+  typedef typename Mma<T>::frag frag;
+  __device__ static __forceinline__ frag tr_load(const T* row_q, const T* row_q4) {
     i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(row_q));
     i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(row_q4));
     typedef __attribute__((ext_vector_type(8))) short i16x8;
     i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(frag, r);
   }
 };
 
@@ -111,7 +110,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const unet_wgrad_desc d, in
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int m0 = wco * 32 + i * 16 + p4;
-          a[i] = WgFrag<bf16>::tr_load(lds_d + pr * RSD + m0, lds_d + (pr + 4) * RSD + m0);
+          a[i] = WgFrag<T>::tr_load(lds_d + pr * RSD + m0, lds_d + (pr + 4) * RSD + m0);
         }
       } else {
 #pragma unroll
@@ -129,7 +128,7 @@ __global__ __launch_bounds__(NTHR) void wgrad_kernel(const unet_wgrad_desc d, in
 #pragma unroll
           for (int j = 0; j < NTN; ++j) {
             const int n0 = wci * (BCI / 2) + j * 16 + p4;
-            b[j] = WgFrag<bf16>::tr_load(lds_x + hp0 * RSX + n0, lds_x + hp1 * RSX + n0);
+            b[j] = WgFrag<T>::tr_load(lds_x + hp0 * RSX + n0, lds_x + hp1 * RSX + n0);
           }
         } else {
           const int p = k0 + (lane >> 4);
@@ -184,7 +183,7 @@ struct WgPlan {
 
 static WgPlan wg_plan(const unet_wgrad_desc* d) {
   WgPlan p;
-  const int kc = d->dtype == UNET_BF16 ? 32 : 16;
+  const int kc = d->dtype != UNET_F32 ? 32 : 16;
   p.tiles_w = cdiv(d->W, TW);
   p.tiles_h = cdiv(d->H, TH);
   p.mtiles = d->N * p.tiles_w * p.tiles_h;
@@ -271,6 +270,7 @@ int unet_conv_wgrad(const unet_wgrad_desc* d, void* stream) {
   if (unet::pw_wgrad_ok(d)) return unet::pw_wgrad(d, st);
   if (unet::wgrad2_eligible(d, nullptr)) return unet::wgrad2_run(d, st);
   if (d->dtype == UNET_BF16) return d->ksize == 3 ? launch_wgrad<bf16, 3>(d, st) : launch_wgrad<bf16, 1>(d, st);
+  if (d->dtype == UNET_F16) return d->ksize == 3 ? launch_wgrad<f16, 3>(d, st) : launch_wgrad<f16, 1>(d, st);
   if (d->dtype == UNET_F32) return d->ksize == 3 ? launch_wgrad<float, 3>(d, st) : launch_wgrad<float, 1>(d, st);
   set_error("unet_conv_wgrad: bad dtype");
   return UNET_ERR_ARG;

@@ -22,12 +22,13 @@ constexpr int W2_RG = 32, W2_RG_MIN = 32;  // two-pass slab reduction above W2_R
 int slab_reduce_two_pass(const float* ws, int splits, long long total, float* scratch, float* dw, int accum,
                          hipStream_t st);  // pw.hip (W2_RG == PW_RG partial slabs)
 
-__device__ __forceinline__ bf16x8 tr8(const bf16* r0, const bf16* r1) {
+template <typename T>
+__device__ __forceinline__ typename Mma<T>::frag tr8(const T* r0, const T* r1) {
   const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r0));
   const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r1));
   // one vector concatenation (lets the two reads land in the halves of one register quad; an element-wise
   // initialiser compiled to v_mov copies)
-  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  return __builtin_bit_cast(typename Mma<T>::frag, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 // compile-time source kinds of the conv input (as conv3's SK): W2_ANY switches per halo item at run time;
@@ -36,21 +37,9 @@ __device__ __forceinline__ bf16x8 tr8(const bf16* r0, const bf16* r1) {
 // goes to LDS as loaded, an activated one is unpacked, transformed and packed once.
 enum { W2_ANY = 0, W2_PLAIN = 1, W2_ACT = 2 };
 
-__device__ __forceinline__ uint4 pack8(const float* v) {
-  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-  unsigned u[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const bf16x2 p = {(__bf16)v[2 * i], (__bf16)v[2 * i + 1]};
-    u[i] = __builtin_bit_cast(unsigned, p);
-  }
-  return make_uint4(u[0], u[1], u[2], u[3]);
-}
-
-template <int KS, int WCO, int WCI, int MI, int RAW, int SK = W2_ANY>
+template <typename T, int KS, int WCO, int WCI, int MI, int RAW, int SK = W2_ANY>
 __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad_desc d, int tiles_w, int tiles_h, int mtiles,
                                                       int per_split, float* ws) {
-  using T = bf16;
   constexpr int W2_NT = 64 * WCO * WCI;
   constexpr int VEC = 8;
   constexpr int BCO = WCO * 16 * MI, BCI = WCI * 16;
@@ -140,7 +129,7 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
           const float gm = sv.gate_p ? sigmoidf_(xg[k] * sv.gate_ab[0] + sv.gate_ab[1]) : 1.f;
 #pragma unroll
           for (int j = 0; j < VEC; ++j) v[j] = inb ? fmaxf(v[j] * sc[j] + sf[j], lo) * gm : 0.f;
-          o = pack8(v);
+          o = pack8_16<T>(v);
         }
         *reinterpret_cast<uint4*>(buf + hp * RSX + vx * VEC) = o;
       }
@@ -231,16 +220,16 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
       const T* dl = bd + (8 * g + q) * RSD + wco * 16 * MI + p4;
       const T* xl0 = bx + ((g >> 1) * HWID + 8 * (g & 1) + q + sw) * RSX + wci * 16 + p4;
       const T* xl1 = bx + ((g >> 1) * HWID + 8 * (g & 1) + q + 4 - sw) * RSX + wci * 16 + p4;
-      bf16x8 a[MI];
+      typename Mma<T>::frag a[MI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) a[i] = tr8(dl + k0 * RSD + i * 16, dl + (k0 + 4) * RSD + i * 16);
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) {
         const int dy = t / KS, dx = t % KS;
         const int off = ((2 * s + dy) * HWID + dx) * RSX;
-        const bf16x8 b = tr8(xl0 + off, xl1 + off);
+        const typename Mma<T>::frag b = tr8(xl0 + off, xl1 + off);
 #pragma unroll
-        for (int i = 0; i < MI; ++i) acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[t][i], 0, 0, 0);
+        for (int i = 0; i < MI; ++i) acc[t][i] = Mma<T>::mma(a[i], b, acc[t][i]);
       }
       if (has_next) {
         if constexpr (RAW == 1) {
@@ -321,7 +310,7 @@ struct W2Plan {
 
 W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   W2Plan p{};
-  p.ok = d->dtype == UNET_BF16 && (d->Cout % 8) == 0;
+  p.ok = d->dtype != UNET_F32 && (d->Cout % 8) == 0;
   p.raw = 1;
   for (int i = 0; i < d->nsrc; ++i) {
     const unet_src& s = d->src[i];
@@ -360,10 +349,10 @@ W2Plan wgrad2_plan(const unet_wgrad_desc* d) {
   return p;
 }
 
-template <int KS, int WCO, int WCI, int MI, int RAW, int SK = W2_ANY>
+template <typename T, int KS, int WCO, int WCI, int MI, int RAW, int SK = W2_ANY>
 static int launch_w2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
   dim3 grid(p.splits, cdiv(d->Cin, WCI * 16), cdiv(d->Cout, WCO * 16 * MI));
-  hipLaunchKernelGGL((wgrad2_kernel<KS, WCO, WCI, MI, RAW, SK>), grid, dim3(64 * WCO * WCI), 0, st, *d, p.tiles_w, p.tiles_h, p.mtiles,
+  hipLaunchKernelGGL((wgrad2_kernel<T, KS, WCO, WCI, MI, RAW, SK>), grid, dim3(64 * WCO * WCI), 0, st, *d, p.tiles_w, p.tiles_h, p.mtiles,
                      p.per_split, (float*)d->workspace);
   return check_launch("wgrad2");
 }
@@ -379,32 +368,37 @@ static int w2_source_kinds(const unet_wgrad_desc* d) {
   return !ok ? W2_ANY : (plain ? W2_PLAIN : W2_ACT);
 }
 
-template <int KS, int RAW>
+template <typename T, int KS, int RAW>
 static int launch_w2_cfg(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
-  if (p.wco == 1) return launch_w2<KS, 1, 4, 4, RAW>(d, p, st);
+  if (p.wco == 1) return launch_w2<T, KS, 1, 4, 4, RAW>(d, p, st);
   if constexpr (KS == 3 && RAW == 1) {
     const int sk = w2_source_kinds(d);
     if (p.wco == 4) {
-      if (sk == W2_PLAIN) return launch_w2<KS, 4, 2, 2, RAW, W2_PLAIN>(d, p, st);
-      if (sk == W2_ACT) return launch_w2<KS, 4, 2, 2, RAW, W2_ACT>(d, p, st);
-      return launch_w2<KS, 4, 2, 2, RAW>(d, p, st);
+      if (sk == W2_PLAIN) return launch_w2<T, KS, 4, 2, 2, RAW, W2_PLAIN>(d, p, st);
+      if (sk == W2_ACT) return launch_w2<T, KS, 4, 2, 2, RAW, W2_ACT>(d, p, st);
+      return launch_w2<T, KS, 4, 2, 2, RAW>(d, p, st);
     }
     if (p.wco == 2 && p.mi == 2) {
-      if (sk == W2_PLAIN) return launch_w2<KS, 2, 4, 2, RAW, W2_PLAIN>(d, p, st);
-      if (sk == W2_ACT) return launch_w2<KS, 2, 4, 2, RAW, W2_ACT>(d, p, st);
-      return launch_w2<KS, 2, 4, 2, RAW>(d, p, st);
+      if (sk == W2_PLAIN) return launch_w2<T, KS, 2, 4, 2, RAW, W2_PLAIN>(d, p, st);
+      if (sk == W2_ACT) return launch_w2<T, KS, 2, 4, 2, RAW, W2_ACT>(d, p, st);
+      return launch_w2<T, KS, 2, 4, 2, RAW>(d, p, st);
     }
   }
   if constexpr (KS == 1) {
-    if (p.wci == 4) return launch_w2<KS, 2, 4, 4, RAW>(d, p, st);
+    if (p.wci == 4) return launch_w2<T, KS, 2, 4, 4, RAW>(d, p, st);
   }
-  return launch_w2<KS, 2, 2, 4, RAW>(d, p, st);
+  return launch_w2<T, KS, 2, 2, 4, RAW>(d, p, st);
 }
 
 int launch_wgrad2(const unet_wgrad_desc* d, const W2Plan& p, hipStream_t st) {
   int e;
-  if (d->ksize == 3) e = p.raw == 4 ? launch_w2_cfg<3, 4>(d, p, st) : launch_w2_cfg<3, 1>(d, p, st);
-  else e = p.raw == 4 ? launch_w2_cfg<1, 4>(d, p, st) : launch_w2_cfg<1, 1>(d, p, st);
+  if (d->dtype == UNET_F16) {
+    if (d->ksize == 3) e = p.raw == 4 ? launch_w2_cfg<f16, 3, 4>(d, p, st) : launch_w2_cfg<f16, 3, 1>(d, p, st);
+    else e = p.raw == 4 ? launch_w2_cfg<f16, 1, 4>(d, p, st) : launch_w2_cfg<f16, 1, 1>(d, p, st);
+  } else {
+    if (d->ksize == 3) e = p.raw == 4 ? launch_w2_cfg<bf16, 3, 4>(d, p, st) : launch_w2_cfg<bf16, 3, 1>(d, p, st);
+    else e = p.raw == 4 ? launch_w2_cfg<bf16, 1, 4>(d, p, st) : launch_w2_cfg<bf16, 1, 1>(d, p, st);
+  }
   if (e) return e;
   const long long total = (long long)d->Cout * d->Cin * d->ksize * d->ksize;
   if (p.splits > W2_RG_MIN && (total & 3) == 0) {

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (import first: libamdhip64.so.7 must resolve to the 
 
 _LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).resolve().parent / "libunet_hip.so"))
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 SRC_PLAIN, SRC_ACT, SRC_POOL_ACT, SRC_UP_ACT, SRC_NCHW_F32, SRC_UP_PLAIN = range(6)
 OUT_Y, OUT_F32, OUT_POOL_BWD, OUT_SHUFFLE2 = range(4)
 

@@ -26,12 +26,14 @@ class Precision:
 
 FP32 = Precision("fp32", L.F32, torch.float32)
 BF16 = Precision("bf16", L.BF16, torch.bfloat16)
-_PRECISIONS = {"fp32": FP32, "float32": FP32, "bf16": BF16, "bfloat16": BF16}
+FP16 = Precision("fp16", L.F16, torch.float16)
+_PRECISIONS = {"fp32": FP32, "float32": FP32, "bf16": BF16, "bfloat16": BF16, "fp16": FP16, "float16": FP16,
+               "half": FP16}
 _default = _PRECISIONS[os.environ.get("UNET_PRECISION", "fp32").lower()]
 
 
 def set_precision(name: str) -> None:
-    """Default operand precision of the HIP kernels ('fp32' = reference numerics, 'bf16')."""
+    """Default operand precision of the HIP kernels ('fp32' = reference numerics, 'bf16', 'fp16')."""
     global _default
     _default = _PRECISIONS[name.lower()]
 

@@ -110,7 +110,7 @@ class ConvBN:
         assert a.has_grad(), "activation gradient missing"
         rows = L.load().unet_bn_bwd_reduce_rows(P, C)
         part = f32(2, rows, C, device=dev)
-        gcode = L.BF16 if a.grad.dtype == torch.bfloat16 else L.F32
+        gcode = {torch.bfloat16: L.BF16, torch.float16: L.F16}.get(a.grad.dtype, L.F32)
         L.call("unet_bn_bwd_reduce", prec.code, gcode, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
                int(a.relu), vp(a.mean), vp(a.invstd), vp(part), stream())
         dgamma, dbeta, coef = f32(C, device=dev), f32(C, device=dev), f32(3, C, device=dev)
@@ -189,10 +189,11 @@ class DoubleConvStage:
 
     def backward(self, prec, grads: Grads, dgrad: Optional[dict]):
         dy2 = self.c2.bn_backward(prec, self.a2, grads)
-        if prec.code == L.BF16:
+        if prec.code != L.F32:
             # the middle activation has one consumer (the second conv): its gradient is written once,
-            # in bf16 (as under torch.autocast), which halves the dgrad store and the BN-backward reads
-            g1 = self.a1.grad_single(torch.bfloat16)
+            # in the 16-bit operand type (as under torch.autocast), which halves the dgrad store and the
+            # BN-backward reads
+            g1 = self.a1.grad_single(prec.torch_dtype)
             self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, {"mode": "y", "out": g1})
         else:
             g1, acc = self.a1.grad_target()
@@ -463,7 +464,7 @@ class DownStage:
         h, w = x.H // 2, x.W // 2
         self.xp = torch.empty(x.N, h, w, x.C, dtype=prec.torch_dtype, device=x.data.device)
         self.code = None
-        vec = 8 if prec.code == L.BF16 else 4
+        vec = 8 if prec.code != L.F32 else 4
         cv = x.C // vec
         if x.C % vec == 0 and cv <= 256 and cv & (cv - 1) == 0:
             # the 2x2 argmax is recorded too: the pool backward then routes by one byte per element

@@ -29,7 +29,17 @@ def confusion_matrix(predictions: torch.Tensor, targets: torch.Tensor, num_class
                      ignore_index: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """int64 [K, K] device tensor, confusion[t, p] (+)= pixel counts (into `out` when given).
 
-    predictions: logits (N, C, H, W) — argmax over dim 1 — or class indices (N, H, W)."""
+    predictions: logits (N, C, H, W) — argmax over dim 1 — or class indices (N, H, W).  Host tensors (what
+    the reference's loop takes) are copied to the current GPU first; the counting always runs in HIP.
+
+    Targets outside [0, K) (and `ignore_index`) are not counted, as in the reference's update()
+    (metrics.py:76-84).  compute_iou / compute_dice inherit this: where the reference's per-class masks
+    would count a pixel with such a target in |pred| (metrics.py:183-188, 217-221), these do not — equal
+    results for targets in [0, K), which is what the reference's datasets produce (binarised masks)."""
+    if not predictions.is_cuda:
+        predictions = predictions.to(f"cuda:{torch.cuda.current_device()}")
+    if targets.device != predictions.device:
+        targets = targets.to(predictions.device)
     require_device(predictions, "predictions")
     require_device(targets, "targets")
     K = int(num_classes)
@@ -78,48 +88,42 @@ class SegmentationMetrics:
         self._cm = None
 
     def update(self, predictions: torch.Tensor, targets: torch.Tensor) -> None:
-        """Add a batch: logits (N, C, H, W) or class indices (N, H, W); targets (N, H, W)."""
-        if self._cm is None or self._cm.device != predictions.device:
+        """Add a batch: logits (N, C, H, W) or class indices (N, H, W); targets (N, H, W).  Host tensors
+        are accepted (copied to the current GPU)."""
+        if not predictions.is_cuda:
+            predictions = predictions.to(f"cuda:{torch.cuda.current_device()}")
+        if self._cm is None:
             self._cm = torch.zeros(self.num_classes, self.num_classes, dtype=torch.int64, device=predictions.device)
+        elif self._cm.device != predictions.device:
+            predictions = predictions.to(self._cm.device)
         confusion_matrix(predictions, targets, self.num_classes, self.ignore_index, out=self._cm)
 
     def compute(self) -> Dict[str, float]:
-        """pixel_accuracy, mean_iou, mean_dice, class_iou, class_dice (metrics.py:86-143)."""
-        cm = self.confusion_matrix
-        total = cm.sum()
-        if total == 0:
-            return self._empty_results()
-        pixel_accuracy = np.diag(cm).sum() / total
-        class_iou, class_dice = {}, {}
-        for i in range(self.num_classes):
-            tp = cm[i, i]
-            fp = cm[:, i].sum() - tp
-            fn = cm[i, :].sum() - tp
-            iou_denom = tp + fp + fn
-            iou = tp / iou_denom if iou_denom > 0 else 0.0
-            dice_denom = 2 * tp + fp + fn
-            dice = 2 * tp / dice_denom if dice_denom > 0 else 0.0
-            class_iou[self.class_names[i]] = iou
-            class_dice[self.class_names[i]] = dice
-        valid_ious = [v for v in class_iou.values() if v > 0]
-        valid_dices = [v for v in class_dice.values() if v > 0]
-        mean_iou = np.mean(valid_ious) if valid_ious else 0.0
-        mean_dice = np.mean(valid_dices) if valid_dices else 0.0
-        return {
-            'pixel_accuracy': float(pixel_accuracy),
-            'mean_iou': float(mean_iou),
-            'mean_dice': float(mean_dice),
-            'class_iou': class_iou,
-            'class_dice': class_dice,
-        }
+        """pixel_accuracy, mean_iou, mean_dice, class_iou, class_dice (metrics.py:86-143).
 
-    def _empty_results(self) -> Dict[str, float]:
+        All classes at once from the matrix: with tp = diag, |pred| = column sums and |true| = row sums,
+        IoU = tp / (|pred| + |true| - tp) and Dice = 2 tp / (|pred| + |true|), 0 where the denominator
+        is 0; the means run over the classes whose score is non-zero.  Integer counts divided in float64,
+        as the reference's per-class scalar arithmetic does, so the values are identical."""
+        cm = self.confusion_matrix
+        names = self.class_names
+        total = int(cm.sum())
+        tp = np.diagonal(cm)
+        both = cm.sum(0) + cm.sum(1)                 # |pred| + |true| per class
+        union, dsum = both - tp, both
+        iou = np.divide(tp, union, out=np.zeros(len(tp)), where=union > 0)
+        dice = np.divide(2 * tp, dsum, out=np.zeros(len(tp)), where=dsum > 0)
+
+        def nz_mean(v):
+            v = v[v > 0]
+            return float(np.mean(v)) if v.size else 0.0
+
         return {
-            'pixel_accuracy': 0.0,
-            'mean_iou': 0.0,
-            'mean_dice': 0.0,
-            'class_iou': {name: 0.0 for name in self.class_names},
-            'class_dice': {name: 0.0 for name in self.class_names},
+            'pixel_accuracy': float(tp.sum() / total) if total else 0.0,
+            'mean_iou': nz_mean(iou) if total else 0.0,
+            'mean_dice': nz_mean(dice) if total else 0.0,
+            'class_iou': dict(zip(names, map(float, iou))),
+            'class_dice': dict(zip(names, map(float, dice))),
         }
 
     def get_confusion_matrix(self) -> np.ndarray:
