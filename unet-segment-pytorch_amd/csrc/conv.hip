@@ -520,33 +520,41 @@ static int dispatch_conv(const unet_conv_desc* d, hipStream_t st) {
 //   transpose=0: rows = Cout, reduction = Cin (forward);
 //   transpose=1: rows = Cin, reduction = Cout, taps flipped 180 degrees (dgrad)
 // ------------------------------------------------------------------------------------------------
+// one 16-byte unit of the packed layout (E16 consecutive K elements of one lane's fragment) per thread:
+// the E16 source values are gathered (L2-resident OIHW rows) and written with a single vector store
+template <typename T>
+__device__ __forceinline__ void pack_unit(const float* w, T* out, int Cout, int Cin, int taps, int transpose,
+                                          int nchunks, long long u) {
+  constexpr int KC = Mma<T>::KC, E16 = 16 / (int)sizeof(T);
+  const int rows = transpose ? Cin : Cout;
+  const int cols = transpose ? Cout : Cin;
+  const int lane = (int)(u % 64);
+  long long t = u / 64;
+  const int tap = (int)(t % taps);
+  t /= taps;
+  const int chunk = (int)(t % nchunks);
+  const int ntile = (int)(t / nchunks);
+  const int r = ntile * 16 + (lane & 15);
+  float v[E16];
+#pragma unroll
+  for (int el = 0; el < E16; ++el) {
+    const int k = (sizeof(T) == 2) ? 8 * (lane >> 4) + el : 4 * el + (lane >> 4);
+    const int cc = chunk * KC + k;
+    v[el] = 0.f;
+    if (r < rows && cc < cols)
+      v[el] = !transpose ? w[((long long)r * Cin + cc) * taps + tap] : w[((long long)cc * Cin + r) * taps + (taps - 1 - tap)];
+  }
+  store_vec<T>(out + u * E16, v);
+}
+
 template <typename T>
 __global__ void pack_kernel(const float* w, T* out, int Cout, int Cin, int ks, int transpose, int rows_pad,
                             int nchunks) {
   constexpr int KC = Mma<T>::KC, E16 = 16 / (int)sizeof(T);
   const int taps = ks * ks;
-  const int rows = transpose ? Cin : Cout;
-  const int cols = transpose ? Cout : Cin;
-  const long long total = (long long)rows_pad * nchunks * KC * taps;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const int el = e % E16;
-    long long t = e / E16;
-    const int lane = t % 64;
-    t /= 64;
-    const int tap = t % taps;
-    t /= taps;
-    const int chunk = t % nchunks;
-    const int ntile = t / nchunks;
-    const int r = ntile * 16 + (lane & 15);
-    const int k = (sizeof(T) == 2) ? 8 * (lane >> 4) + el : 4 * el + (lane >> 4);
-    const int cc = chunk * KC + k;
-    float v = 0.f;
-    if (r < rows && cc < cols) {
-      if (!transpose) v = w[((long long)r * Cin + cc) * taps + tap];
-      else v = w[((long long)cc * Cin + r) * taps + (taps - 1 - tap)];
-    }
-    out[e] = from_f<T>(v);
-  }
+  const long long units = (long long)rows_pad * nchunks * KC * taps / E16;
+  for (long long u = blockIdx.x * (long long)blockDim.x + threadIdx.x; u < units; u += (long long)gridDim.x * blockDim.x)
+    pack_unit<T>(w, out, Cout, Cin, taps, transpose, nchunks, u);
 }
 
 // many weights in one launch: job table passed by value in the kernel arguments; blockIdx.y = job
@@ -563,27 +571,9 @@ __global__ void pack_many_kernel(const PackJobs jobs) {
   const int cols = jb.transpose ? jb.Cout : jb.Cin;
   const int rows_pad = (rows + PACK_NPAD - 1) / PACK_NPAD * PACK_NPAD;
   const int nchunks = (cols + KC - 1) / KC;
-  const long long total = (long long)rows_pad * nchunks * KC * taps;
-  T* out = (T*)jb.packed;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const int el = e % E16;
-    long long t = e / E16;
-    const int lane = t % 64;
-    t /= 64;
-    const int tap = t % taps;
-    t /= taps;
-    const int chunk = t % nchunks;
-    const int ntile = t / nchunks;
-    const int r = ntile * 16 + (lane & 15);
-    const int k = (sizeof(T) == 2) ? 8 * (lane >> 4) + el : 4 * el + (lane >> 4);
-    const int cc = chunk * KC + k;
-    float v = 0.f;
-    if (r < rows && cc < cols) {
-      if (!jb.transpose) v = jb.w[((long long)r * jb.Cin + cc) * taps + tap];
-      else v = jb.w[((long long)cc * jb.Cin + r) * taps + (taps - 1 - tap)];
-    }
-    out[e] = from_f<T>(v);
-  }
+  const long long units = (long long)rows_pad * nchunks * KC * taps / E16;
+  for (long long u = blockIdx.x * (long long)blockDim.x + threadIdx.x; u < units; u += (long long)gridDim.x * blockDim.x)
+    pack_unit<T>(jb.w, (T*)jb.packed, jb.Cout, jb.Cin, taps, jb.transpose, nchunks, u);
 }
 
 static int packed_rows(int Cout, int Cin, int transpose) {
@@ -654,7 +644,8 @@ int unet_pack_weights(int dtype, int count, const unet_pack_job* jobs, void* str
     const long long e = unet_packed_weight_elems(dtype, j.Cout, j.Cin, j.ksize, j.transpose);
     if (e > maxe) maxe = e;
   }
-  int blocks = (int)((maxe + 255) / 256);
+  const long long maxu = maxe / (dtype != UNET_F32 ? 8 : 4);   // 16-byte units
+  int blocks = (int)((maxu + 255) / 256);
   if (blocks > 1024) blocks = 1024;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == UNET_F16)
@@ -678,7 +669,7 @@ int unet_pack_weight(int dtype, const float* w, void* packed, int Cout, int Cin,
   const int kc = dtype != UNET_F32 ? 32 : 16;
   const int rows_pad = packed_rows(Cout, Cin, transpose);
   const int nchunks = cdiv(transpose ? Cout : Cin, kc);
-  const long long total = (long long)rows_pad * nchunks * kc * ksize * ksize;
+  const long long total = (long long)rows_pad * nchunks * kc * ksize * ksize / (dtype != UNET_F32 ? 8 : 4);
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   if (dtype == UNET_F16)
