@@ -84,6 +84,19 @@ typedef struct unet_conv_desc {
   const float* bias;      /* SHUFFLE2: fp32 [Ct] (may be NULL)                                     */
   const uint8_t* pool_code; /* POOL_BWD, optional: 2x2 argmax (0..3, row-major) per pooled element and
                              channel [N,H,W,Cout], as written by unet_materialize_pool             */
+  /* Y mode, optional — the BatchNorm backward reduction of the activation whose gradient this conv
+   * writes (a dgrad with a single consumer; replaces the Σ passes of BatchNorm2d's backward,
+   * layers.py:33-37): with g = out (as stored) where relu?(bnb_y*bnb_scale+bnb_shift) > 0, else 0,
+   * bnb_stats[r][Cout] = Σ g and bnb_stats[rows + r][Cout] = Σ g·(bnb_y − bnb_mean)·bnb_invstd over the
+   * r-th of rows = unet_conv_stats_rows(d) pixel tiles (ask with bnb_y set; reduce the two
+   * [rows][Cout] arrays with unet_bn_bwd_finalize).                                                 */
+  const void* bnb_y;      /* op dtype [N,H,W,Cout]: the activation's stored conv output            */
+  const float* bnb_scale; /* its BN affine (scale, shift), ReLU flag and batch statistics          */
+  const float* bnb_shift;
+  int bnb_relu;
+  const float* bnb_mean;
+  const float* bnb_invstd;
+  float* bnb_stats;       /* NULL: no reduction                                                    */
 } unet_conv_desc;
 
 typedef struct unet_wgrad_desc {

@@ -699,3 +699,57 @@ def test_wgrad_source_kinds(prec, shape, kind):
     torch.cuda.synchronize()
     rel = float((dw - ref).double().norm() / ref.double().norm())
     assert rel <= 2e-3, rel    # the gate / activation rounding to bf16 can differ by one ulp from torch's
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("shape", [(4, 256, 256, 64, 64), (4, 128, 128, 128, 128), (2, 64, 64, 256, 256),
+                                   (1, 24, 40, 64, 64), (2, 20, 36, 36, 20), (3, 33, 20, 96, 128)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_dgrad_y_bn_backward_sums(prec, shape):
+    """The dgrad y epilogue's fused BatchNorm-backward reduction (unet_conv_desc.bnb_*): per channel
+    Σg and Σg·(y-mean)·invstd of the STORED gradient g, masked by the activation's ReLU, against torch
+    on the same stored values (conv3 / conv2 epilogues and the fallback reduction of the other paths)."""
+    L, R = _lib(), _rt()
+    N, H, W, cmid, cout = shape     # the conv cmid -> cout; its dgrad writes the cmid-channel gradient
+    dt = DT[prec]
+    torch.manual_seed(21)
+    dy = _rand(N, H, W, cout, dt=dt)
+    w = (torch.randn(cout, cmid, 3, 3, device="cuda") * (2.0 / (9 * cmid)) ** 0.5).to(dt).float()
+    y1 = _rand(N, H, W, cmid, dt=dt)
+    sc = torch.rand(cmid, device="cuda") + 0.5
+    sf = torch.randn(cmid, device="cuda") * 0.3
+    ab = torch.stack([sc, sf])
+    mean = torch.randn(cmid, device="cuda") * 0.1
+    invstd = torch.rand(cmid, device="cuda") + 0.5
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    g = torch.empty(N, H, W, cmid, dtype=dt, device="cuda")
+    P = R._PRECISIONS[prec]
+    wp = R.pack_weight(w, P, transpose=True)
+    d = L.ConvDesc()
+    d.dtype = P.code
+    d.N, d.H, d.W, d.Cin, d.Cout, d.ksize, d.nsrc = N, H, W, cout, cmid, 3, 1
+    d.src[0] = src
+    d.weight = wp.data_ptr()
+    d.out_mode = L.OUT_Y
+    d.out = g.data_ptr()
+    d.bnb_y, d.bnb_scale, d.bnb_shift, d.bnb_relu = y1.data_ptr(), ab[0].data_ptr(), ab[1].data_ptr(), 1
+    d.bnb_mean, d.bnb_invstd = mean.data_ptr(), invstd.data_ptr()
+    rows = L.load().unet_conv_stats_rows(d)
+    part = torch.full((2, rows, cmid), float("nan"), device="cuda")
+    d.bnb_stats = part.data_ptr()
+    L.call("unet_conv", d, R.stream())
+    torch.cuda.synchronize()
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
+    _close_bf16(g.float(), ref, "dgrad y")
+    gs = g.double().reshape(-1, cmid)
+    yv = y1.double().reshape(-1, cmid)
+    mask = (yv * sc.double() + sf.double()) > 0
+    gm = torch.where(mask, gs, torch.zeros_like(gs))
+    s1 = gm.sum(0)
+    s2 = (gm * (yv - mean.double()) * invstd.double()).sum(0)
+    got = part.double().sum(1)
+    assert torch.isfinite(got).all(), _variant(d)
+    for k, (a, b) in enumerate(((got[0], s1), (got[1], s2))):
+        scale = gm.abs().sum(0) * (1 if k == 0 else float((yv - mean.double()).abs().max() * invstd.max()))
+        assert ((a - b).abs() <= 1e-5 * scale + 1e-4).all(), (k, float((a - b).abs().max()), _variant(d))

@@ -590,7 +590,14 @@ static const char* tname(int dtype) { return dtype == UNET_BF16 ? "bf16" : dtype
 
 int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8); }
 
+// does unet_conv reduce d's bnb_* sums in the conv epilogue (rows = the conv's M tiles)?
+static bool bnb_in_epilogue(const unet_conv_desc* d) {
+  if (smallcin_conv_ok(d) || pw_conv_ok(d) || !fast_eligible(d) || d->dtype == UNET_F32) return false;
+  return conv3_bnb_tile(d, pick_cfg(d));
+}
+
 int unet_conv_stats_rows(const unet_conv_desc* d) {
+  if (d->bnb_y && !bnb_in_epilogue(d)) return unet_bn_bwd_reduce_rows((long long)d->N * d->H * d->W, d->Cout);
   if (smallcin_conv_ok(d)) return smallcin_rows((long long)d->N * d->H * d->W);
   if (pw_conv_ok(d)) return pw_conv_rows(d);
   if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
@@ -718,14 +725,25 @@ int unet_conv(const unet_conv_desc* d, void* stream) {
     set_error("unet_conv: bad pool_src");
     return UNET_ERR_ARG;
   }
+  if (d->bnb_stats && (d->out_mode != UNET_OUT_Y || d->stats || !d->bnb_y || !d->bnb_scale || !d->bnb_shift ||
+                       !d->bnb_mean || !d->bnb_invstd)) {
+    set_error("unet_conv: bnb_stats needs the y mode, no forward stats and every bnb_* pointer");
+    return UNET_ERR_ARG;
+  }
+  if (d->dtype != UNET_BF16 && d->dtype != UNET_F16 && d->dtype != UNET_F32) {
+    set_error("unet_conv: bad dtype");
+    return UNET_ERR_ARG;
+  }
   hipStream_t st = (hipStream_t)stream;
-  if (smallcin_conv_ok(d)) return smallcin_conv(d, st);
-  if (pw_conv_ok(d)) return pw_conv(d, st);
-  if (d->dtype == UNET_BF16) return dispatch_conv<bf16>(d, st);
-  if (d->dtype == UNET_F16) return dispatch_conv<f16>(d, st);
-  if (d->dtype == UNET_F32) return dispatch_conv<float>(d, st);
-  set_error("unet_conv: bad dtype");
-  return UNET_ERR_ARG;
+  int rc;
+  if (smallcin_conv_ok(d)) rc = smallcin_conv(d, st);
+  else if (pw_conv_ok(d)) rc = pw_conv(d, st);
+  else rc = UNET_DISPATCH_T(d->dtype, dispatch_conv<T>(d, st));
+  if (rc || !d->bnb_stats || bnb_in_epilogue(d)) return rc;
+  // the other paths: the separate BatchNorm-backward reduction over the stored gradient
+  return unet_bn_bwd_reduce(d->dtype, d->dtype, (long long)d->N * d->H * d->W, d->Cout, d->out, d->bnb_y,
+                            d->bnb_scale, d->bnb_shift, d->bnb_relu, d->bnb_mean, d->bnb_invstd, d->bnb_stats,
+                            stream);
 }
 
 }  // extern "C"

@@ -50,4 +50,25 @@ template <typename T> __host__ __device__ constexpr int kc_of() { return sizeof(
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 __device__ __forceinline__ int round_up_d(int a, int b) { return (a + b - 1) / b * b; }
 
+
+// internal output mode of the conv kernels: the y epilogue of a dgrad that also reduces the BatchNorm
+// backward sums of the activation it is the gradient of (unet_conv_desc.bnb_*)
+constexpr int OM_Y_BNB = 8;
+
+// 4 x 16-bit values (8 bytes) -> 4 floats
+template <typename T>
+__device__ __forceinline__ void unpack4_16(const uint2& q, float* v) {
+  if constexpr (__is_same(T, bf16)) {
+    v[0] = __uint_as_float(q.x << 16);
+    v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16);
+    v[3] = __uint_as_float(q.y & 0xffff0000u);
+  } else {
+    typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+    const f16x4 h = __builtin_bit_cast(f16x4, q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (float)h[i];
+  }
+}
+
 }  // namespace unet

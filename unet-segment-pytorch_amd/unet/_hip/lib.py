@@ -31,7 +31,9 @@ class ConvDesc(ctypes.Structure):
     _fields_ = [("dtype", c_int), ("N", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
                 ("ksize", c_int), ("nsrc", c_int), ("src", Src * 2), ("weight", c_vp), ("out_mode", c_int),
                 ("out", c_vp), ("out2", c_vp), ("split", c_int), ("accum", c_int), ("accum2", c_int),
-                ("stats", c_vp), ("pool_src", Src), ("bias", c_vp), ("pool_code", c_vp)]
+                ("stats", c_vp), ("pool_src", Src), ("bias", c_vp), ("pool_code", c_vp),
+                ("bnb_y", c_vp), ("bnb_scale", c_vp), ("bnb_shift", c_vp), ("bnb_relu", c_int), ("bnb_mean", c_vp),
+                ("bnb_invstd", c_vp), ("bnb_stats", c_vp)]
 
 
 class PackJob(ctypes.Structure):

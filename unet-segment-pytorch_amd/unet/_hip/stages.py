@@ -103,16 +103,20 @@ class ConvBN:
         return a
 
     # ---- backward ----
-    def bn_backward(self, prec: Precision, a: Act, grads: Grads) -> torch.Tensor:
-        """BatchNorm2d(+ReLU) backward: returns dy (op dtype, NHWC) at the conv output."""
+    def bn_backward(self, prec: Precision, a: Act, grads: Grads, fused=None) -> torch.Tensor:
+        """BatchNorm2d(+ReLU) backward: returns dy (op dtype, NHWC) at the conv output.  `fused`: the
+        (partial sums [2][rows][C], rows) the producing dgrad's epilogue already reduced (bnb_*)."""
         dev = a.data.device
         P, C = a.pixels, a.C
         assert a.has_grad(), "activation gradient missing"
-        rows = L.load().unet_bn_bwd_reduce_rows(P, C)
-        part = f32(2, rows, C, device=dev)
         gcode = {torch.bfloat16: L.BF16, torch.float16: L.F16}.get(a.grad.dtype, L.F32)
-        L.call("unet_bn_bwd_reduce", prec.code, gcode, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
-               int(a.relu), vp(a.mean), vp(a.invstd), vp(part), stream())
+        if fused is not None:
+            part, rows = fused
+        else:
+            rows = L.load().unet_bn_bwd_reduce_rows(P, C)
+            part = f32(2, rows, C, device=dev)
+            L.call("unet_bn_bwd_reduce", prec.code, gcode, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]),
+                   vp(a.ab[1]), int(a.relu), vp(a.mean), vp(a.invstd), vp(part), stream())
         dgamma, dbeta, coef = f32(C, device=dev), f32(C, device=dev), f32(3, C, device=dev)
         L.call("unet_bn_bwd_finalize", vp(part[0]), vp(part[1]), rows, C, P, vp(self.bn.weight), vp(a.mean),
                vp(a.invstd), vp(dgamma), vp(dbeta), 0, vp(coef), stream())
@@ -152,9 +156,18 @@ class ConvBN:
         self.pre_wt = None
         d = _conv_desc(prec, N, H, W, self.cout, self.cin, self.k, [_plain_src(dy)], wt)
         if dgrad["mode"] == "y":
-            # op-dtype gradient, stored (the y epilogue without BN sums)
+            # op-dtype gradient, stored; with "bnb" (the Act it is the gradient of) the epilogue also
+            # reduces that activation's BatchNorm-backward sums, returned in dgrad["bnb_part"]
             d.out_mode = L.OUT_Y
             d.out = dgrad["out"].data_ptr()
+            a = dgrad.get("bnb")
+            if a is not None:
+                d.bnb_y, d.bnb_scale, d.bnb_shift = vp(a.data), vp(a.ab[0]), vp(a.ab[1])
+                d.bnb_relu, d.bnb_mean, d.bnb_invstd = int(a.relu), vp(a.mean), vp(a.invstd)
+                rows = L.load().unet_conv_stats_rows(d)
+                part = f32(2, rows, self.cin, device=dev)
+                d.bnb_stats = part.data_ptr()
+                dgrad["bnb_part"] = (part, rows)
         elif dgrad["mode"] == "pool":
             d.out_mode = L.OUT_POOL_BWD
             d.out = dgrad["out"].data_ptr()
@@ -193,13 +206,17 @@ class DoubleConvStage:
             # the middle activation has one consumer (the second conv): its gradient is written once,
             # in the 16-bit operand type (as under torch.autocast), which halves the dgrad store and the
             # BN-backward reads
+            # BN1's backward sums are reduced by that dgrad's epilogue (no separate pass over g1 and y1)
             g1 = self.a1.grad_single(prec.torch_dtype)
-            self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, {"mode": "y", "out": g1})
+            route = {"mode": "y", "out": g1, "bnb": self.a1 if self.a1.mean is not None else None}
+            self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, route)
+            fused = route.get("bnb_part")
         else:
             g1, acc = self.a1.grad_target()
             self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, {"mode": "f32", "out": g1, "accum": acc})
+            fused = None
         del dy2
-        dy1 = self.c1.bn_backward(prec, self.a1, grads)
+        dy1 = self.c1.bn_backward(prec, self.a1, grads, fused)
         self.c1.conv_backward(prec, dy1, self.srcs, grads, dgrad)
 
 
