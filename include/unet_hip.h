@@ -175,6 +175,13 @@ int unet_bn_bwd_apply(int dtype, int da_dtype, long long P, int C, const void* d
 int unet_gate_psi_rows(long long P);
 int unet_gate_psi(int dtype, long long P, int Ci, const void* gw, const void* xw, const float* gab,
                   const float* xab, const float* wpsi, float* p, float* partial, void* stream);
+/* eval mode in one pass (scripts/predict.py): p = sum_c wpsi_c * relu(sg*(W_g.g)+bg + sx*(W_x.x)+bx)
+ * straight from g (stored, at x's size) and x = relu?(y*xs+xb), W_g / W_x packed (transpose=0);
+ * gab / xab: [2][Ci] eval BN affines.  16-bit operands, Cg, Cx, Ci divisible by 32               */
+int unet_gate_psi_eval(int dtype, long long P, int Cg, int Cx, int Ci, const void* g, const void* x,
+                       const float* xs, const float* xb, int xrelu, const void* wg_packed,
+                       const void* wx_packed, const float* gab, const float* xab, const float* wpsi,
+                       float* p, void* stream);
 /* backward 1: x = ACT(y_x); s = sigmoid(psi BN(p)); ds = sum_c d_c x_c; dx (+)= d*s; dq = ds s (1-s) */
 int unet_gate_bwd1(int dtype, long long P, int Cx, const float* dxs, const void* yx, const float* sx,
                    const float* bx, int relu, const float* p, const float* psi_ab, const float* psi_mean,

@@ -753,3 +753,35 @@ def test_dgrad_y_bn_backward_sums(prec, shape):
     for k, (a, b) in enumerate(((got[0], s1), (got[1], s2))):
         scale = gm.abs().sum(0) * (1 if k == 0 else float((yv - mean.double()).abs().max() * invstd.max()))
         assert ((a - b).abs() <= 1e-5 * scale + 1e-4).all(), (k, float((a - b).abs().max()), _variant(d))
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("shape", [(2, 64, 64, 512, 512, 256), (2, 96, 80, 64, 64, 32), (1, 33, 47, 128, 128, 64)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_gate_psi_eval_single_pass(prec, shape):
+    """unet_gate_psi_eval (the eval-mode AttentionGate in one pass, layers.py:171-192 with running-stat
+    BN) against torch fp32 on the same 16-bit inputs: p = wpsi . relu(bn_g(W_g g) + bn_x(W_x relu(bn(y))))."""
+    L, R = _lib(), _rt()
+    N, H, W, cg, cx, ci = shape
+    dt = DT[prec]
+    torch.manual_seed(31)
+    g = _rand(N, H, W, cg, dt=dt)
+    y = _rand(N, H, W, cx, dt=dt)
+    xab = torch.stack([torch.rand(cx, device="cuda") + 0.5, torch.randn(cx, device="cuda") * 0.2])
+    wg = (torch.randn(ci, cg, 1, 1, device="cuda") * cg ** -0.5).to(dt).float()
+    wx = (torch.randn(ci, cx, 1, 1, device="cuda") * cx ** -0.5).to(dt).float()
+    gab = torch.stack([torch.rand(ci, device="cuda") + 0.5, torch.randn(ci, device="cuda") * 0.2])
+    pab = torch.stack([torch.rand(ci, device="cuda") + 0.5, torch.randn(ci, device="cuda") * 0.2])
+    wpsi = torch.randn(ci, device="cuda") * ci ** -0.5
+    P = R._PRECISIONS[prec]
+    wgp, wxp = R.pack_weight(wg, P, transpose=False), R.pack_weight(wx, P, transpose=False)
+    p = torch.full((N, H, W), float("nan"), device="cuda")
+    L.call("unet_gate_psi_eval", P.code, N * H * W, cg, cx, ci, g.data_ptr(), y.data_ptr(), xab[0].data_ptr(),
+           xab[1].data_ptr(), 1, wgp.data_ptr(), wxp.data_ptr(), gab.data_ptr(), pab.data_ptr(), wpsi.data_ptr(),
+           p.data_ptr(), R.stream())
+    torch.cuda.synchronize()
+    x = (y.float() * xab[0] + xab[1]).clamp_min(0).to(dt).float()      # the kernel feeds 16-bit x to the MFMA
+    a = (g.float() @ wg.view(ci, cg).t()) * gab[0] + gab[1] + (x @ wx.view(ci, cx).t()) * pab[0] + pab[1]
+    ref = a.clamp_min(0) @ wpsi
+    rel = float((p - ref).norm() / ref.norm())
+    assert torch.isfinite(p).all() and rel <= 1e-4, rel     # fp32 accumulation: summation order only

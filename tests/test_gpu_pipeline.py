@@ -108,3 +108,33 @@ def test_graphed_predictor_matches_eager_and_predict_masks():
     assert torch.equal(masks, ref)
     assert torch.allclose(ratio, (ref > 127).float().mean((1, 2)))
     assert masks.shape == (2, 300, 300) and masks.dtype == torch.uint8
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_eval_single_pass_gate_in_the_network(prec):
+    """model.eval() under no_grad takes the one-pass attention gate (unet_gate_psi_eval); with autograd
+    enabled it keeps the two-pass training form.  Both against the fp64 oracle's eval logits: the
+    one-pass form (projections never rounded to 16 bits) is no less accurate."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from oracle import unet_oracle as O
+    from unet.models import AttentionUNet
+    torch.manual_seed(0)
+    m = AttentionUNet(1, 2).cuda()
+    m.hip_precision = prec
+    m.train()
+    with torch.no_grad():
+        m(torch.rand(2, 1, 64, 64, device="cuda") * 2 - 1)     # non-trivial running statistics
+    m.eval()
+    x = torch.rand(2, 1, 64, 64, device="cuda") * 2 - 1
+    with torch.no_grad():
+        one = m(x).double()
+    two = m(x).detach().double()                                # grad enabled: two-pass gate
+    p = {k: v.detach().double().cuda() for k, v in m.state_dict().items()}
+    ref = O.attention_unet_forward(p, x.double(), training=False)
+    e1 = float((one - ref).norm() / ref.norm())
+    e2 = float((two - ref).norm() / ref.norm())
+    print(f"\n{prec} eval logits rel-L2 vs fp64: one-pass gate {e1:.3e}, two-pass {e2:.3e}")
+    assert e1 <= 1.1 * e2 + 1e-3 and e1 <= 2e-2, (e1, e2)
+    assert not torch.equal(one, two)        # the one-pass kernel did run

@@ -72,6 +72,8 @@ _SIGS = {
     "unet_colsum": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp]),
     "unet_gate_psi_rows": (c_int, [c_ll]),
     "unet_gate_psi": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "unet_gate_psi_eval": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
+                                   c_vp, c_vp, c_vp, c_vp]),
     "unet_gate_bwd1": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
                                c_vp, c_vp, c_vp]),
     "unet_gate_bwd2_rows": (c_int, [c_ll, c_int]),

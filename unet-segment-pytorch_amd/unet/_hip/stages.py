@@ -231,10 +231,17 @@ class GateStage:
         self.psi_conv, self.psi_bn = m.psi[0], m.psi[1]
         self.ci = self.cg.cout
 
-    def forward(self, prec, g: Act, x: Act, training: bool, g_up: Optional[L.Src] = None):
+    def forward(self, prec, g: Act, x: Act, training: bool, g_up: Optional[L.Src] = None,
+                g_up_t: Optional[torch.Tensor] = None):
         N, H, W = x.N, x.H, x.W
         dev = x.data.device
         self.g, self.x = g, x
+        # g_up_t is given only for an untracked eval-mode forward (no backward follows)
+        if (not training and g_up_t is not None and prec.code != L.F32
+                and self.psi_bn.track_running_stats and self.cg.bn.track_running_stats
+                and self.cx.bn.track_running_stats and g.C % 32 == 0 and x.C % 32 == 0 and self.ci % 32 == 0):
+            self._forward_eval(prec, g_up_t, x)
+            return
         # bilinear(g -> x size) (layers.py:183): the Up stage's materialised map when it is the same one
         self.src_g = g_up if g_up is not None else g.src_up(H, W, 0, 0)
         self.gw = self.cg.forward(prec, [self.src_g], N, H, W, training)
@@ -261,6 +268,28 @@ class GateStage:
         else:
             L.call("unet_bn_eval_affine", 1, vp(bn.weight), vp(bn.bias), vp(bn.running_mean), vp(bn.running_var),
                    float(bn.eps), vp(self.psi_ab[0]), vp(self.psi_ab[1]), stream())
+
+    def _forward_eval(self, prec, g_up_t: torch.Tensor, x: Act):
+        """Eval mode, no autograd (predict.py): BN on running statistics, so psi's pre-activation is
+        computed in one pass from g_up and x (unet_gate_psi_eval) without storing W_g(g) / W_x(x)."""
+        dev = x.data.device
+        ci = self.ci
+        wg = self.cg.pre_wp if self.cg.pre_wp is not None else pack_weight(self.cg.conv.weight, prec, False)
+        wx = self.cx.pre_wp if self.cx.pre_wp is not None else pack_weight(self.cx.conv.weight, prec, False)
+        self.cg.pre_wp = self.cx.pre_wp = None
+        gab, xab = f32(2, ci, device=dev), f32(2, ci, device=dev)
+        for bn, ab in ((self.cg.bn, gab), (self.cx.bn, xab)):
+            L.call("unet_bn_eval_affine", ci, vp(bn.weight), vp(bn.bias), vp(bn.running_mean), vp(bn.running_var),
+                   float(bn.eps), vp(ab[0]), vp(ab[1]), stream())
+        self.wpsi = self.psi_conv.weight.detach().reshape(-1).float().contiguous()
+        self.p = f32(x.N, x.H, x.W, device=dev)
+        L.call("unet_gate_psi_eval", prec.code, x.pixels, g_up_t.shape[-1], x.C, ci, vp(g_up_t), vp(x.data),
+               vp(x.ab[0]), vp(x.ab[1]), int(x.relu), vp(wg), vp(wx), vp(gab), vp(xab), vp(self.wpsi),
+               vp(self.p), stream())
+        bn = self.psi_bn
+        self.psi_ab = f32(2, 1, device=dev)
+        L.call("unet_bn_eval_affine", 1, vp(bn.weight), vp(bn.bias), vp(bn.running_mean), vp(bn.running_var),
+               float(bn.eps), vp(self.psi_ab[0]), vp(self.psi_ab[1]), stream())
 
     def gated_src(self) -> L.Src:
         return self.x.src_gated(self.p, self.psi_ab)
@@ -416,7 +445,7 @@ class UpStage:
         self.dc = DoubleConvStage(m.conv)
         self.gate = GateStage(m.attention) if attention else None
 
-    def forward(self, prec, x1: Act, x2: Act, training: bool) -> Act:
+    def forward(self, prec, x1: Act, x2: Act, training: bool, eval_only: bool = False) -> Act:
         self.x1, self.x2 = x1, x2
         self.geo = _pad_geometry(x1, x2)
         up_h, up_w, pt, pl = self.geo
@@ -427,7 +456,8 @@ class UpStage:
             self.up_t = up_t
         if self.gate is not None:
             same = up_t is not None and up_h == x2.H and up_w == x2.W and pt == 0 and pl == 0
-            self.gate.forward(prec, x1, x2, training, g_up=_plain_src(up_t) if same else None)
+            self.gate.forward(prec, x1, x2, training, g_up=_plain_src(up_t) if same else None,
+                              g_up_t=up_t if same and eval_only else None)
             skip = self.gate.gated_src()
         else:
             skip = x2.src()
@@ -590,8 +620,9 @@ class NetworkPlan:
         return out
 
     # ---- forward pieces ----
-    def begin(self, prec: Precision, x: torch.Tensor, training: bool, need_dx: bool):
+    def begin(self, prec: Precision, x: torch.Tensor, training: bool, need_dx: bool, tracked: bool = True):
         self.prec, self.training, self.x, self.need_dx = prec, training, x, need_dx
+        self.tracked = tracked   # False: no backward will follow (the eval-only kernels may be used)
         self.with_ds = self.ds and training
         self._bwd_packed = False
         cbs = self.convbns()
@@ -608,7 +639,8 @@ class NetworkPlan:
 
     def fwd_up(self, i: int):
         y = self.xs[4] if i == 0 else self.dec[-1]
-        self.dec.append(self.ups[i].forward(self.prec, y, self.xs[3 - i], self.training))   # d4, d3, d2, d1
+        self.dec.append(self.ups[i].forward(self.prec, y, self.xs[3 - i], self.training,   # d4, d3, d2, d1
+                                            eval_only=not self.tracked))
 
     def fwd_outc(self) -> torch.Tensor:
         return self.outc.forward(self.prec, self.dec[-1])
@@ -620,7 +652,7 @@ class NetworkPlan:
 
     def forward(self, prec: Precision, x: torch.Tensor, training: bool, need_dx: bool):
         """The whole forward in one go (no autograd: eval / no_grad)."""
-        self.begin(prec, x, training, need_dx)
+        self.begin(prec, x, training, need_dx, tracked=False)
         self.fwd_inc()
         for i in range(4):
             self.fwd_down(i)
