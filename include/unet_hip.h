@@ -255,6 +255,11 @@ int unet_materialize_pool(int dtype, const unet_src* src, long long N, int H, in
 int unet_confusion_matrix(long long N, int K, long long HW, const float* logits, const int64_t* labels,
                           const int64_t* targets, long long ignore_index, int has_ignore, int64_t* confusion,
                           void* stream);
+/* compute_iou / compute_dice, metrics.py:160-231: a (K+1) x (K+1) matrix (int64, accumulated) whose
+ * row / column K counts targets / predictions outside [0, K), so every pixel lands once and
+ * |pred == c| / |target == c| are the column / row sums; logits have C channels (C may differ from K). */
+int unet_confusion_matrix_ext(long long N, int C, int K, long long HW, const float* logits, const int64_t* labels,
+                              const int64_t* targets, int64_t* confusion, void* stream);
 
 /* ---- DiceBCE / Dice / BalancedCE loss + grad — loss.py:18-191 ------------------------------- */
 int unet_loss_rows(long long HW);

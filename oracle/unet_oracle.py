@@ -201,6 +201,18 @@ def confusion_matrix(pred_labels: torch.Tensor, t: torch.Tensor, num_classes: in
     return torch.bincount(k, minlength=num_classes * num_classes).reshape(num_classes, num_classes)
 
 
+def class_iou_dice(pred_labels: torch.Tensor, t: torch.Tensor, num_classes: int = 2, smooth: float = 1e-6):
+    """compute_iou / compute_dice — metrics.py:178-192, 213-227: per class, boolean masks over every pixel
+    (targets outside [0, K) included), float32 sums, (I + s) / (U + s) and (2I + s) / (|p| + |t| + s)."""
+    iou, dice = [], []
+    for c in range(num_classes):
+        pc, tc = pred_labels == c, t == c
+        inter = (pc & tc).float().sum()
+        iou.append((inter + smooth) / ((pc | tc).float().sum() + smooth))
+        dice.append((2.0 * (pc.float() * tc.float()).sum() + smooth) / (pc.float().sum() + tc.float().sum() + smooth))
+    return torch.stack(iou), torch.stack(dice)
+
+
 def segmentation_scores(cm: np.ndarray, class_names) -> dict:
     """SegmentationMetrics.compute — metrics.py:86-143: per class c, tp = cm[c, c], fp = column c minus tp,
     fn = row c minus tp; IoU = tp / (tp + fp + fn), Dice = 2 tp / (2 tp + fp + fn) (0 for a zero

@@ -83,3 +83,26 @@ def test_metrics_accept_host_tensors():
     assert np.array_equal(m.get_confusion_matrix(), (O.confusion_matrix(z.argmax(1), t, 2) * 2).numpy())
     assert m.compute() == O.segmentation_scores(m.get_confusion_matrix(), m.class_names)
     assert torch.equal(compute_dice(z, t).cpu(), compute_dice(z.cuda(), t.cuda()).cpu())
+
+
+@pytest.mark.parametrize("C,K", [(2, 2), (3, 2), (2, 3)])
+def test_iou_dice_count_every_pixel(C, K):
+    """compute_iou / compute_dice with targets outside [0, K) (an ignore label 255, a stray 7) and logits
+    whose channel count C differs from num_classes: the reference's per-class masks count such pixels in
+    |pred == c| (metrics.py:183-188, 217-221); the extended (K+1)^2 matrix does the same."""
+    from unet.utils.metrics import compute_dice, compute_iou
+    O = _o()
+    gen = torch.Generator().manual_seed(14 + C * 3 + K)
+    z = torch.randn(3, C, 45, 61, generator=gen)
+    t = torch.randint(0, K, (3, 45, 61), generator=gen)
+    t[0, :6] = 255
+    t[2, :, :4] = 7
+    t[1, 3, 5] = -1
+    ri, rd = O.class_iou_dice(z.argmax(1), t, K)
+    assert torch.equal(compute_iou(z.cuda(), t.cuda(), K).cpu(), ri)
+    assert torch.equal(compute_dice(z.cuda(), t.cuda(), K).cpu(), rd)
+    # class-index predictions, including labels >= K
+    p = z.argmax(1)
+    ri, rd = O.class_iou_dice(p, t, K)
+    assert torch.equal(compute_iou(p.cuda(), t.cuda(), K).cpu(), ri)
+    assert torch.equal(compute_dice(p, t, K).cpu(), rd)

@@ -101,6 +101,7 @@ _SIGS = {
     "unet_materialize": (c_int, [c_int, ctypes.POINTER(Src), c_ll, c_int, c_int, c_vp, c_vp]),
     "unet_materialize_pool": (c_int, [c_int, ctypes.POINTER(Src), c_ll, c_int, c_int, c_vp, c_vp, c_vp]),
     "unet_confusion_matrix": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp]),
+    "unet_confusion_matrix_ext": (c_int, [c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "unet_loss_rows": (c_int, [c_ll]),
     "unet_loss_reduce": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp]),
     "unet_loss_finalize": (c_int, [c_vp, c_int, c_ll, c_int, c_float, c_float, c_float, c_float, c_float, c_int, c_int,

@@ -33,9 +33,7 @@ def confusion_matrix(predictions: torch.Tensor, targets: torch.Tensor, num_class
     the reference's loop takes) are copied to the current GPU first; the counting always runs in HIP.
 
     Targets outside [0, K) (and `ignore_index`) are not counted, as in the reference's update()
-    (metrics.py:76-84).  compute_iou / compute_dice inherit this: where the reference's per-class masks
-    would count a pixel with such a target in |pred| (metrics.py:183-188, 217-221), these do not — equal
-    results for targets in [0, K), which is what the reference's datasets produce (binarised masks)."""
+    (metrics.py:76-84).  (compute_iou / compute_dice count every pixel instead: `_class_counts`.)"""
     if not predictions.is_cuda:
         predictions = predictions.to(f"cuda:{torch.cuda.current_device()}")
     if targets.device != predictions.device:
@@ -132,10 +130,34 @@ class SegmentationMetrics:
 
 
 def _class_counts(predictions: torch.Tensor, targets: torch.Tensor, num_classes: int):
-    cm = confusion_matrix(predictions, targets, num_classes).to(torch.float32)
-    tp = torch.diagonal(cm)
-    pred = cm.sum(0)     # pixels predicted as class c
-    true = cm.sum(1)     # pixels labelled class c
+    """(|pred ∩ target|, |pred|, |target|) per class c < num_classes over EVERY pixel, as the reference's
+    per-class masks count them (metrics.py:183-188, 217-221): one `unet_confusion_matrix_ext` launch
+    into a (K+1) x (K+1) matrix whose last row / column holds targets / predictions outside [0, K)
+    (e.g. an ignore label 255, or argmax classes >= K when the logits have C != K channels)."""
+    if not predictions.is_cuda:
+        predictions = predictions.to(f"cuda:{torch.cuda.current_device()}")
+    if targets.device != predictions.device:
+        targets = targets.to(predictions.device)
+    require_device(predictions, "predictions")
+    K = int(num_classes)
+    t = targets.to(torch.int64).contiguous()
+    if predictions.dim() == 4:
+        z = predictions.detach().float().contiguous()
+        N, C, H, W = z.shape
+        logits, labels, P = z.data_ptr(), None, N * H * W
+    else:
+        p = predictions.detach().to(torch.int64).contiguous()
+        N, C, P = p.shape[0], 0, p.numel()
+        logits, labels = None, p.data_ptr()
+    if t.numel() != P:
+        raise ValueError(f"targets have {t.numel()} elements, predictions describe {P} pixels")
+    cm = torch.zeros(K + 1, K + 1, dtype=torch.int64, device=predictions.device)
+    L.call("unet_confusion_matrix_ext", N, C, K, P // max(N, 1), logits, labels, t.data_ptr(), cm.data_ptr(),
+           stream())
+    cm = cm.to(torch.float32)
+    tp = torch.diagonal(cm)[:K]
+    pred = cm.sum(0)[:K]     # pixels predicted as class c (any target)
+    true = cm.sum(1)[:K]     # pixels labelled class c (any prediction)
     return tp, pred, true
 
 
