@@ -169,6 +169,18 @@ int unet_colsum(const float* part, int rows, int C, float* out, int accum, void*
 /* dy (op dtype) = A*g + B*y + Cc                                                                */
 int unet_bn_bwd_apply(int dtype, int da_dtype, long long P, int C, const void* da, const void* y,
                       const float* scale, const float* shift, int relu, const float* coef, void* dy, void* stream);
+/* the same two passes for a Down block's input activation (N, H, W, C; C % 8 == 0, C/8 a power of two),
+ * whose MaxPool2d(2) backward (layers.py:56) is folded in: g = da (fp32, NULL = no other consumer) +
+ * g2[n][h/2][w/2][c] where code[n][h/2][w/2][c] == 2*(h&1) + (w&1) (g2: fp32 [N][ph][pw][C], the Down
+ * conv's dgrad; code: unet_materialize_pool's argmax codes).  Replaces the pool-routing dgrad epilogue's
+ * read-modify-write of the full-resolution gradient.                                             */
+int unet_bn_bwd_reduce_pool(int dtype, long long N, int H, int W, int C, const float* da, const float* g2,
+                            const uint8_t* code, int ph, int pw, const void* y, const float* scale,
+                            const float* shift, int relu, const float* mean, const float* invstd, float* partial,
+                            void* stream);
+int unet_bn_bwd_apply_pool(int dtype, long long N, int H, int W, int C, const float* da, const float* g2,
+                           const uint8_t* code, int ph, int pw, const void* y, const float* scale, const float* shift,
+                           int relu, const float* coef, void* dy, void* stream);
 
 /* ---- attention gate (AttentionGate.forward/backward) — layers.py:171-192 ---------------------- */
 /* p = sum_c wpsi_c * relu(sg*gw+bg + sx*xw+bx) ; partial sums of p                               */

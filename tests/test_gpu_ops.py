@@ -785,3 +785,54 @@ def test_gate_psi_eval_single_pass(prec, shape):
     ref = a.clamp_min(0) @ wpsi
     rel = float((p - ref).norm() / ref.norm())
     assert torch.isfinite(p).all() and rel <= 1e-4, rel     # fp32 accumulation: summation order only
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("shape", [(4, 512, 512, 64), (2, 21, 20, 64), (3, 34, 19, 128), (1, 6, 7, 1024)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("with_da", [True, False])
+def test_bn_backward_pooled_gradient(prec, shape, with_da):
+    """unet_bn_bwd_reduce_pool / _apply_pool (a Down block's MaxPool2d backward folded into the producer's
+    BatchNorm backward) against the plain passes on the explicitly routed full-resolution gradient
+    da + unpool(g2, code) — the same fp32 additions in the same order, so bit-identical; odd H / W
+    leave the last row / column without a pooled contribution (MaxPool2d floors)."""
+    L, R = _lib(), _rt()
+    N, H, W, C = shape
+    dt = DT[prec]
+    ph, pw = H // 2, W // 2
+    torch.manual_seed(23)
+    y = _rand(N, H, W, C, dt=dt)
+    da = torch.randn(N, H, W, C, device="cuda") if with_da else None
+    g2 = torch.randn(N, ph, pw, C, device="cuda")
+    code = torch.randint(0, 4, (N, ph, pw, C), dtype=torch.uint8, device="cuda")
+    sc = torch.rand(C, device="cuda") + 0.5
+    sf = torch.randn(C, device="cuda") * 0.3
+    ab = torch.stack([sc, sf]).contiguous()
+    mean = torch.randn(C, device="cuda") * 0.1
+    invstd = torch.rand(C, device="cuda") + 0.5
+    # the routed reference gradient
+    full = da.clone() if with_da else torch.zeros(N, H, W, C, device="cuda")
+    for q in range(4):
+        a, b = q >> 1, q & 1
+        sl = full[:, a:2 * ph:2, b:2 * pw:2, :]
+        sl += torch.where(code == q, g2, torch.zeros_like(g2))
+    P = N * H * W
+    pc = R._PRECISIONS[prec].code
+    rows = L.load().unet_bn_bwd_reduce_rows(P, C)
+    part_ref = torch.empty(2, rows, C, device="cuda")
+    part = torch.empty(2, rows, C, device="cuda")
+    vp = R.vp
+    L.call("unet_bn_bwd_reduce", pc, L.F32, P, C, vp(full), vp(y), vp(ab[0]), vp(ab[1]), 1, vp(mean), vp(invstd),
+           vp(part_ref), R.stream())
+    L.call("unet_bn_bwd_reduce_pool", pc, N, H, W, C, vp(da) if with_da else None, vp(g2), vp(code), ph, pw, vp(y),
+           vp(ab[0]), vp(ab[1]), 1, vp(mean), vp(invstd), vp(part), R.stream())
+    coef = torch.randn(3, C, device="cuda")
+    dy_ref = torch.empty(N, H, W, C, dtype=dt, device="cuda")
+    dy = torch.empty_like(dy_ref)
+    L.call("unet_bn_bwd_apply", pc, L.F32, P, C, vp(full), vp(y), vp(ab[0]), vp(ab[1]), 1, vp(coef), vp(dy_ref),
+           R.stream())
+    L.call("unet_bn_bwd_apply_pool", pc, N, H, W, C, vp(da) if with_da else None, vp(g2), vp(code), ph, pw, vp(y),
+           vp(ab[0]), vp(ab[1]), 1, vp(coef), vp(dy), R.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(part, part_ref)
+    assert torch.equal(dy, dy_ref)

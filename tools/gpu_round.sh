@@ -12,7 +12,7 @@ timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "
 cat $O/bench.json
 timeout -k 10 300 python -u bench.py --precision fp16 --in-ch 3 --size 1024 --accum 8 --steps 2 --warmup 1 --no-cpu-baseline --no-fp32-line > $O/bench_c5.json 2> $O/bench_c5.err || { echo "c5 bench failed"; tail -20 $O/bench_c5.err; exit 1; }
 cat $O/bench_c5.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/trace.log 2>&1 || { echo "trace failed"; tail -20 $O/trace.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp32-line > $O/trace.log 2>&1 || { echo "trace failed"; tail -20 $O/trace.log; exit 1; }
 timeout -k 10 200 python -u tools/layerprof.py > $O/layerprof.txt 2>&1 || { echo "layerprof failed"; tail -20 $O/layerprof.txt; exit 1; }
 i=0
 for set in FETCH_SIZE WRITE_SIZE; do

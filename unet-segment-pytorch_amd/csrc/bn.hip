@@ -156,13 +156,46 @@ template <typename G> __device__ __forceinline__ void load8(const G* p, float* v
   if constexpr (sizeof(G) == 4) load_vec<G>(p + 4, v + 4);
 }
 
+// The MaxPool2d(2) backward of a Down block's input, left at the pooled resolution: the Down's first-conv
+// dgrad writes g2 (fp32 [N][ph][pw][C], plain stores) and the materialised pool's argmax codes (uint8, same
+// shape, q = 2*dy + dx in the window) route it here.  Full-resolution element (n, h, w, c) receives
+// g2[n][h/2][w/2][c] where code == 2*(h&1) + (w&1) (rows / columns past 2*ph, 2*pw: none), added after the
+// other consumers' sum `da` — the order and values of the RMW the pool-routing dgrad epilogue did
+// (layers.py:56, MaxPool2d backward), without that epilogue's read-modify-write of the full map.
+struct PoolG {
+  const float* g2;
+  const uint8_t* code;
+  int H, W, ph, pw;
+};
+
+// (32-bit index math: the host admits N*H*W < 2^31; a 64-bit division here cost half the bandwidth)
+__device__ __forceinline__ void pool_add8(const PoolG& pg, int C, long long p, int c0, float* g) {
+  const unsigned pu = (unsigned)p, W = (unsigned)pg.W, H = (unsigned)pg.H;
+  const unsigned t = pu / W, w = pu - t * W;
+  const unsigned n = t / H, h = t - n * H;
+  const unsigned hh = h >> 1, ww = w >> 1;
+  if (hh >= (unsigned)pg.ph || ww >= (unsigned)pg.pw) return;
+  const size_t o = (size_t)((n * (unsigned)pg.ph + hh) * (unsigned)pg.pw + ww) * C + c0;
+  const uint2 cw = *reinterpret_cast<const uint2*>(pg.code + o);
+  const float4 a = *reinterpret_cast<const float4*>(pg.g2 + o);
+  const float4 b = *reinterpret_cast<const float4*>(pg.g2 + o + 4);
+  const unsigned q = (unsigned)((h & 1) * 2 + (w & 1));
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned cj = ((j < 4 ? cw.x : cw.y) >> (8 * (j & 3))) & 0xffu;
+    if (cj == q) g[j] += v[j];
+  }
+}
+
 // vectorised forms (C % 8 == 0): a thread owns 8 channels (16-byte y, 2 x 16-byte da) of one pixel;
-// the block covers 256 / (C/8) pixels per iteration with a fixed channel vector per thread
-template <typename T, typename G>
+// the block covers 256 / (C/8) pixels per iteration with a fixed channel vector per thread.
+// POOL: + the pooled gradient (PoolG); da may then be null (no other consumer)
+template <typename T, typename G, bool POOL = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int C, const G* da, const T* y,
                                                                 const float* scale, const float* shift, int relu,
                                                                 const float* mean, const float* invstd, float* part,
-                                                                int rows) {
+                                                                int rows, PoolG pg = PoolG{}) {
   __shared__ float sh[2][256 * 8 / 8];
   const int CV = C / 8, tid = threadIdx.x;
   const int cv = tid % CV, py = tid / CV, R = 256 / CV;
@@ -180,7 +213,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int
       float yv[8], g[8];
       load_vec<T>(y + p * C + cv * 8, yv);
       if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
-      load8<G>(da + p * C + cv * 8, g);
+      if (!POOL || da) {
+        load8<G>(da + p * C + cv * 8, g);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = 0.f;
+      }
+      if constexpr (POOL) pool_add8(pg, C, p, cv * 8, g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[j];
@@ -205,10 +244,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int
   }
 }
 
-template <typename T, typename G>
+template <typename T, typename G, bool POOL = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int C, const G* da, const T* y,
                                                                const float* scale, const float* shift, int relu,
-                                                               const float* coef, T* dy) {
+                                                               const float* coef, T* dy, PoolG pg = PoolG{}) {
   const int CV = C / 8;
   const long long total = P * CV;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -226,7 +265,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int 
     float yv[8], g[8], o[8];
     load_vec<T>(y + p * C + cv * 8, yv);
     if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
-    load8<G>(da + p * C + cv * 8, g);
+    if (!POOL || da) {
+      load8<G>(da + p * C + cv * 8, g);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = 0.f;
+    }
+    if constexpr (POOL) pool_add8(pg, C, p, cv * 8, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[j];
@@ -438,6 +483,57 @@ int unet_bn_bwd_apply(int dtype, int da_dtype, long long P, int C, const void* d
     hipLaunchKernelGGL((bn_bwd_apply_kernel<float, float>), grid, dim3(256), 0, st, P, C, cl, (const float*)da,
                        (const float*)y, scale, shift, relu, coef, (float*)dy, rows);
   return check_launch("bn_bwd_apply");
+}
+
+// BN backward of a Down block's input activation with the pooled gradient folded in (PoolG above)
+int unet_bn_bwd_reduce_pool(int dtype, long long N, int H, int W, int C, const float* da, const float* g2,
+                            const uint8_t* code, int ph, int pw, const void* y, const float* scale,
+                            const float* shift, int relu, const float* mean, const float* invstd, float* partial,
+                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long long P = N * H * W;
+  if (!bn_vec_ok(C) || !g2 || !code || P <= 0 || P >= (1LL << 31) || ph > (H >> 1) || pw > (W >> 1) || ph < 0 ||
+      pw < 0) {
+    set_error("unet_bn_bwd_reduce_pool: bad arguments (C % 8 == 0, C/8 a power of two <= 256)");
+    return UNET_ERR_ARG;
+  }
+  const PoolG pg{g2, code, H, W, ph, pw};
+  const int rows = reduce_rows_vec(P, C);
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<f16, float, true>), dim3(rows), dim3(256), 0, st, P, C, da,
+                       (const f16*)y, scale, shift, relu, mean, invstd, partial, rows, pg);
+  else if (dtype == UNET_BF16)
+    hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<bf16, float, true>), dim3(rows), dim3(256), 0, st, P, C, da,
+                       (const bf16*)y, scale, shift, relu, mean, invstd, partial, rows, pg);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<float, float, true>), dim3(rows), dim3(256), 0, st, P, C, da,
+                       (const float*)y, scale, shift, relu, mean, invstd, partial, rows, pg);
+  return check_launch("bn_bwd_reduce_pool");
+}
+
+int unet_bn_bwd_apply_pool(int dtype, long long N, int H, int W, int C, const float* da, const float* g2,
+                           const uint8_t* code, int ph, int pw, const void* y, const float* scale, const float* shift,
+                           int relu, const float* coef, void* dy, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long long P = N * H * W;
+  if (!bn_vec_ok(C) || !g2 || !code || P <= 0 || P >= (1LL << 31) || ph > (H >> 1) || pw > (W >> 1) || ph < 0 ||
+      pw < 0) {
+    set_error("unet_bn_bwd_apply_pool: bad arguments (C % 8 == 0, C/8 a power of two <= 256)");
+    return UNET_ERR_ARG;
+  }
+  const PoolG pg{g2, code, H, W, ph, pw};
+  long long b = (P * (C / 8) + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<f16, float, true>), dim3((int)b), dim3(256), 0, st, P, C, da,
+                       (const f16*)y, scale, shift, relu, coef, (f16*)dy, pg);
+  else if (dtype == UNET_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<bf16, float, true>), dim3((int)b), dim3(256), 0, st, P, C, da,
+                       (const bf16*)y, scale, shift, relu, coef, (bf16*)dy, pg);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<float, float, true>), dim3((int)b), dim3(256), 0, st, P, C, da,
+                       (const float*)y, scale, shift, relu, coef, (float*)dy, pg);
+  return check_launch("bn_bwd_apply_pool");
 }
 
 int unet_colsum(const float* part, int rows, int C, float* out, int accum, void* stream) {

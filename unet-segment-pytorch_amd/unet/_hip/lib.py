@@ -69,6 +69,10 @@ _SIGS = {
     "unet_bn_bwd_reduce": (c_int, [c_int, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "unet_bn_bwd_finalize": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "unet_bn_bwd_apply": (c_int, [c_int, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "unet_bn_bwd_reduce_pool": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
+                                        c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "unet_bn_bwd_apply_pool": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
+                                       c_vp, c_int, c_vp, c_vp, c_vp]),
     "unet_colsum": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp]),
     "unet_gate_psi_rows": (c_int, [c_ll]),
     "unet_gate_psi": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

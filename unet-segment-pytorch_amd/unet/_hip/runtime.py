@@ -183,7 +183,8 @@ class Act:
     `grad` is the NHWC gradient w.r.t. that activation, accumulated by its consumers: fp32, or bf16
     for a single-consumer activation in bf16 mode (`grad_single`)."""
 
-    __slots__ = ("data", "N", "H", "W", "C", "ab", "relu", "mean", "invstd", "grad", "_grad_init", "keep")
+    __slots__ = ("data", "N", "H", "W", "C", "ab", "relu", "mean", "invstd", "grad", "_grad_init", "keep",
+                 "bn_owned", "pool_grad")
 
     def __init__(self, data: torch.Tensor, ab: Optional[torch.Tensor], relu: bool,
                  mean: Optional[torch.Tensor] = None, invstd: Optional[torch.Tensor] = None):
@@ -196,6 +197,10 @@ class Act:
         self.grad = None
         self._grad_init = False
         self.keep = None
+        # set by ConvBN.forward: the gradient is consumed by that ConvBN's BatchNorm backward, which can
+        # fold a Down block's pooled gradient (pool_grad = (g2, code, ph, pw)) in on the fly
+        self.bn_owned = False
+        self.pool_grad = None
 
     @property
     def scale(self):

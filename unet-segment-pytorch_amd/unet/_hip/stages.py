@@ -100,6 +100,7 @@ class ConvBN:
                    vp(bn.running_var), float(bn.eps), vp(ab[0]), vp(ab[1]), stream())
         a = Act(y, ab, self.relu, mean, invstd)
         a.keep = keep  # keeps the source tensors alive until backward
+        a.bn_owned = True
         return a
 
     # ---- backward ----
@@ -108,9 +109,20 @@ class ConvBN:
         (partial sums [2][rows][C], rows) the producing dgrad's epilogue already reduced (bnb_*)."""
         dev = a.data.device
         P, C = a.pixels, a.C
-        assert a.has_grad(), "activation gradient missing"
-        gcode = {torch.bfloat16: L.BF16, torch.float16: L.F16}.get(a.grad.dtype, L.F32)
-        if fused is not None:
+        pool = a.pool_grad
+        assert a.has_grad() or pool is not None, "activation gradient missing"
+        gcode = {torch.bfloat16: L.BF16, torch.float16: L.F16}.get(a.grad.dtype, L.F32) if a.has_grad() else L.F32
+        if pool is not None:
+            # a Down block's input: its MaxPool2d backward is folded into both passes (the pooled dgrad is
+            # routed by the argmax codes and added after the other consumers' fp32 sum)
+            assert fused is None and gcode == L.F32
+            g2, code, ph, pw = pool
+            da = vp(a.grad) if a.has_grad() else None
+            rows = L.load().unet_bn_bwd_reduce_rows(P, C)
+            part = f32(2, rows, C, device=dev)
+            L.call("unet_bn_bwd_reduce_pool", prec.code, a.N, a.H, a.W, C, da, vp(g2), vp(code), ph, pw,
+                   vp(a.data), vp(a.ab[0]), vp(a.ab[1]), int(a.relu), vp(a.mean), vp(a.invstd), vp(part), stream())
+        elif fused is not None:
             part, rows = fused
         else:
             rows = L.load().unet_bn_bwd_reduce_rows(P, C)
@@ -123,8 +135,13 @@ class ConvBN:
         grads.put(self.bn.weight, dgamma)
         grads.put(self.bn.bias, dbeta)
         dy = torch.empty(a.N, a.H, a.W, C, dtype=prec.torch_dtype, device=dev)
-        L.call("unet_bn_bwd_apply", prec.code, gcode, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
-               int(a.relu), vp(coef), vp(dy), stream())
+        if pool is not None:
+            L.call("unet_bn_bwd_apply_pool", prec.code, a.N, a.H, a.W, C, da, vp(g2), vp(code), ph, pw, vp(a.data),
+                   vp(a.ab[0]), vp(a.ab[1]), int(a.relu), vp(coef), vp(dy), stream())
+            a.pool_grad = None
+        else:
+            L.call("unet_bn_bwd_apply", prec.code, gcode, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+                   int(a.relu), vp(coef), vp(dy), stream())
         return dy
 
     def conv_backward(self, prec: Precision, dy: torch.Tensor, srcs: List[L.Src], grads: Grads,
@@ -522,8 +539,20 @@ class DownStage:
         return self.dc.forward(prec, [_plain_src(self.xp)], x.N, h, w, training)
 
     def backward(self, prec, grads: Grads):
-        g = self.x.grad_zeroed()
-        self.dc.backward(prec, grads, {"mode": "pool", "out": g, "pool_src": self.x.src_pool(), "code": self.code})
+        x = self.x
+        cv = x.C // 8
+        if self.code is not None and x.bn_owned and x.C % 8 == 0 and cv <= 256 and cv & (cv - 1) == 0 \
+                and x.pixels < 2 ** 31 and x.pool_grad is None and (x.grad is None or x.grad.dtype == torch.float32):
+            # the dgrad is written at the pooled resolution (plain fp32 stores); the producer's BatchNorm
+            # backward routes it through the argmax codes while it reads the other consumers' gradient
+            # (unet_bn_bwd_reduce_pool / _apply_pool), so the full-resolution map is never read-modified
+            h, w = self.xp.shape[1], self.xp.shape[2]
+            g2 = f32(x.N, h, w, x.C, device=x.data.device)
+            self.dc.backward(prec, grads, {"mode": "f32", "out": g2, "accum": 0})
+            x.pool_grad = (g2, self.code, h, w)
+            return
+        g = x.grad_zeroed()
+        self.dc.backward(prec, grads, {"mode": "pool", "out": g, "pool_src": x.src_pool(), "code": self.code})
 
 
 class OutConvStage:
