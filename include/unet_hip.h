@@ -61,9 +61,14 @@ enum {
   UNET_OUT_Y = 0,         /* store y (op dtype, NHWC) + per-tile BN partial sums                  */
   UNET_OUT_F32 = 1,       /* fp32 NHWC; split channels [0,split) -> out, [split,Cout) -> out2      */
   UNET_OUT_POOL_BWD = 2,  /* route to the 2x2 argmax of pool_src (ACT), add into out (fp32)        */
-  UNET_OUT_SHUFFLE2 = 3   /* ConvTranspose2d(k=2, s=2) as a 1x1 conv with Cout = 4*Ct: output channel
+  UNET_OUT_SHUFFLE2 = 3,  /* ConvTranspose2d(k=2, s=2) as a 1x1 conv with Cout = 4*Ct: output channel
                              (2a+b)*Ct + c of pixel (y, x) -> out[n, 2y+a, 2x+b, c] + bias[c]
                              (op dtype [N,2H,2W,Ct])                         — layers.py:81,218   */
+  UNET_OUT_F32_GATED = 4  /* the attention gate's W_x input gradient with the x*s term fused in
+                             (layers.py:171-192): out[px][c] (+)= sigmoid(pool_src.gate_p[px] *
+                             pool_src.gate_ab[0] + gate_ab[1]) * pool_src.data[px][c] + (W^T dy)[px][c];
+                             pool_src.data = d(x*s), fp32 NHWC [N,H,W,Cout]; split == Cout; `accum` as
+                             F32.  Served by the bf16 1x1 path only (unet_conv_variant "pw_conv_kernel")*/
 };
 
 typedef struct unet_conv_desc {
@@ -194,7 +199,8 @@ int unet_gate_psi_eval(int dtype, long long P, int Cg, int Cx, int Ci, const voi
                        const float* xs, const float* xb, int xrelu, const void* wg_packed,
                        const void* wx_packed, const float* gab, const float* xab, const float* wpsi,
                        float* p, void* stream);
-/* backward 1: x = ACT(y_x); s = sigmoid(psi BN(p)); ds = sum_c d_c x_c; dx (+)= d*s; dq = ds s (1-s) */
+/* backward 1: x = ACT(y_x); s = sigmoid(psi BN(p)); ds = sum_c d_c x_c; dx (+)= d*s; dq = ds s (1-s)
+ * (dx may be NULL: the d*s term then goes through the W_x dgrad, UNET_OUT_F32_GATED)             */
 int unet_gate_bwd1(int dtype, long long P, int Cx, const float* dxs, const void* yx, const float* sx,
                    const float* bx, int relu, const float* p, const float* psi_ab, const float* psi_mean,
                    const float* psi_invstd, float* dx, int dx_accum, float* dq, float* partial, void* stream);

@@ -836,3 +836,54 @@ def test_bn_backward_pooled_gradient(prec, shape, with_da):
     torch.cuda.synchronize()
     assert torch.equal(part, part_ref)
     assert torch.equal(dy, dy_ref)
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 128, 64, 32), (4, 181, 183, 64, 64), (4, 200, 170, 32, 64)],
+                         ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("accum", [0, 1])
+def test_pw_dgrad_gated(shape, accum):
+    """UNET_OUT_F32_GATED: the attention gate's W_x input gradient with the x*s term fused in,
+    out (+)= sigmoid(p*a+b) * d(x*s) + W_x^T dy (layers.py:171-192), against torch; the pass-1 kernel then
+    writes no dx (unet_gate_bwd1 with dx = NULL)."""
+    L, R = _lib(), _rt()
+    N, H, W, cin, cout = shape     # forward 1x1 conv cin (= Cx) -> cout (= Ci); dgrad dy[cout] -> dx[cin]
+    dt = torch.bfloat16
+    torch.manual_seed(7)
+    dy = _rand(N, H, W, cout, dt=dt)
+    w = (torch.randn(cout, cin, 1, 1, device="cuda") * 0.1).to(dt).float()
+    dxs = torch.randn(N, H, W, cin, device="cuda")
+    p = torch.randn(N, H, W, device="cuda")
+    ab = torch.tensor([0.7, -0.2], device="cuda")
+    old = torch.randn(N, H, W, cin, device="cuda")
+    out = old.clone()
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    ps = L.Src()
+    ps.kind, ps.C, ps.H, ps.W = L.SRC_PLAIN, cin, H, W
+    ps.data, ps.gate_p, ps.gate_ab = dxs.data_ptr(), p.data_ptr(), ab.data_ptr()
+    d = _conv("bf16", [src], N, H, W, cout, w, 1, L.OUT_F32_GATED, transpose=True, out=out.data_ptr(),
+              split=cin, accum=accum, pool_src=ps)
+    assert _pw_var(L, d).startswith("pw_conv_kernel"), _pw_var(L, d)
+    s = torch.sigmoid(p * ab[0] + ab[1]).unsqueeze(-1)
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w).permute(0, 2, 3, 1) + dxs * s
+    if accum:
+        ref = ref + old
+    assert (out - ref).abs().max() <= 2e-2 * (1 + ref.abs().max())
+    # pass 1 without dx: dq and the psi-BN sums unchanged, nothing written to dx
+    R_ = _rt()
+    y = _rand(N, H, W, cin, dt=dt)
+    sc, sf = torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.1
+    pm, pi = torch.zeros(1, device="cuda"), torch.ones(1, device="cuda")
+    P = N * H * W
+    rows = L.load().unet_gate_psi_rows(P)
+    dq1, dq2 = torch.empty(P, device="cuda"), torch.empty(P, device="cuda")
+    part1, part2 = torch.empty(2, rows, device="cuda"), torch.empty(2, rows, device="cuda")
+    dx = torch.empty(N, H, W, cin, device="cuda")
+    vp = R_.vp
+    L.call("unet_gate_bwd1", L.BF16, P, cin, vp(dxs), vp(y), vp(sc), vp(sf), 1, vp(p), vp(ab), vp(pm), vp(pi), vp(dx),
+           0, vp(dq1), vp(part1), R_.stream())
+    L.call("unet_gate_bwd1", L.BF16, P, cin, vp(dxs), vp(y), vp(sc), vp(sf), 1, vp(p), vp(ab), vp(pm), vp(pi), None,
+           0, vp(dq2), vp(part2), R_.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dq1, dq2) and torch.equal(part1, part2)
+    assert torch.allclose(dx, dxs * s, rtol=1e-6, atol=1e-6)

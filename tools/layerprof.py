@@ -17,7 +17,7 @@ from unet._hip import lib as L  # noqa: E402
 from unet._hip.runtime import conv_kernel_name  # noqa: E402
 
 KIND = {0: "plain", 1: "act", 2: "pool", 3: "up", 4: "nchw", 5: "upplain"}
-OUT = {0: "y", 1: "f32", 2: "poolbwd", 3: "shuf2"}
+OUT = {0: "y", 1: "f32", 2: "poolbwd", 3: "shuf2", 4: "f32gate"}
 
 _orig = L.call
 _rec = []

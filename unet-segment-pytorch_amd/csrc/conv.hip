@@ -715,7 +715,16 @@ int unet_conv(const unet_conv_desc* d, void* stream) {
     set_error("unet_conv: bad split");
     return UNET_ERR_ARG;
   }
-  if (d->out_mode < UNET_OUT_Y || d->out_mode > UNET_OUT_SHUFFLE2 ||
+  if (d->out_mode == UNET_OUT_F32_GATED) {
+    if (!d->pool_src.data || !d->pool_src.gate_p || !d->pool_src.gate_ab || d->split != d->Cout) {
+      set_error("unet_conv: F32_GATED needs pool_src.data / gate_p / gate_ab and split == Cout");
+      return UNET_ERR_ARG;
+    }
+    if (!pw_conv_ok(d)) {
+      set_error("unet_conv: F32_GATED is served by the bf16 1x1 path only");
+      return UNET_ERR_UNSUPPORTED;
+    }
+  } else if (d->out_mode < UNET_OUT_Y || d->out_mode > UNET_OUT_SHUFFLE2 ||
       (d->out_mode == UNET_OUT_SHUFFLE2 && (d->Cout % 4 || d->ksize != 1))) {
     set_error("unet_conv: bad out_mode");
     return UNET_ERR_ARG;

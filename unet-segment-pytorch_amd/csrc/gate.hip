@@ -84,15 +84,17 @@ __global__ void gate_bwd1_kernel(long long P, int Cx, const float* dxs, const T*
     const float sg = sigmoidf_(pv * pa + pb);
     const float* d = dxs + q * Cx;
     const T* y = yx + q * Cx;
-    float* o = dx + q * Cx;
+    float* o = dx ? dx + q * Cx : nullptr;
     float ds = 0.f;
     for (int c = 0; c < Cx; ++c) {
       float xv = to_f(y[c]) * sx[c] + bx[c];
       if (relu) xv = fmaxf(xv, 0.f);
       const float dv = d[c];
       ds += dv * xv;
-      const float g = dv * sg;
-      o[c] = dx_accum ? o[c] + g : g;
+      if (dx) {
+        const float g = dv * sg;
+        o[c] = dx_accum ? o[c] + g : g;
+      }
     }
     const float dqv = ds * sg * (1.f - sg);
     dq[q] = dqv;
@@ -192,7 +194,7 @@ __global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* dx
       load_vec<float>(dxs + qq * Cx + c0 + 4, d[u] + 4);
       load8<T>(yx + qq * Cx + c0, y[u]);
       pv[u] = pp[qq];
-      if (dx_accum) {
+      if (dx && dx_accum) {
         load_vec<float>(dx + qq * Cx + c0, g[u]);
         load_vec<float>(dx + qq * Cx + c0 + 4, g[u] + 4);
       }
@@ -217,9 +219,11 @@ __global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* dx
       ds = group_sum(ds, G);
       if (ok[u]) {
         const long long qq = q + u * S;
-        float* o = dx + qq * Cx + c0;
-        store_vec<float>(o, g[u]);
-        store_vec<float>(o + 4, g[u] + 4);
+        if (dx) {  // null: the x*s term is added by the W_x dgrad (UNET_OUT_F32_GATED)
+          float* o = dx + qq * Cx + c0;
+          store_vec<float>(o, g[u]);
+          store_vec<float>(o + 4, g[u] + 4);
+        }
         if (sub == 0) {
           const float dqv = ds * sg * (1.f - sg);
           dq[qq] = dqv;

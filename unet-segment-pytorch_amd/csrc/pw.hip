@@ -57,7 +57,9 @@ __device__ __forceinline__ bf16x8 pw_act(uint4 q, bool act, const float* sc, con
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad.  Block = 4 waves; wave = 16*NB pixels x 16*NA output channels; grid (P / (64*NB), Cout / (16*NA))
 // ------------------------------------------------------------------------------------------------
-template <int NA, int NB>
+// GATED (UNET_OUT_F32_GATED): the attention gate's W_x input gradient, with the x*s term of the same
+// gradient added here instead of by gate_bwd1: d(x*s) and s = sigmoid(psi) are loaded ahead of the MFMAs
+template <int NA, int NB, bool GATED = false>
 __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, long long P, int nchunks) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i16 = lane & 15, g = lane >> 4;
@@ -93,6 +95,43 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
   uint4 xq[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) xq[b] = pw_ld(xr, xoff[b], 0);
+  // fp32 gradient epilogue that accumulates: the old values are loaded here, ahead of the MFMAs (the
+  // compiler cannot hoist them over the stores, which it must assume alias; loaded in the epilogue, each
+  // read-modify-write was a full memory round trip per 16-byte column)
+  float4 old[NB][NA];
+  const bool rmw = !GATED && d.out_mode == UNET_OUT_F32 && (d.accum || d.accum2);
+  float4 gxs[GATED ? NB : 1][GATED ? NA : 1];
+  float gsv[GATED ? NB : 1];
+  if constexpr (GATED) {
+    const float* dxs = (const float*)d.pool_src.data;
+    const float ga = d.pool_src.gate_ab[0], gb = d.pool_src.gate_ab[1];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const long long p = pw0 + 16 * b + i16;
+      gsv[b] = p < P ? sigmoidf_(d.pool_src.gate_p[p] * ga + gb) : 0.f;
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        gxs[b][a] = p < P ? *reinterpret_cast<const float4*>(dxs + p * d.Cout + co0 + 16 * a + 4 * g)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if (rmw) {
+    const int c2 = d.Cout - d.split;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const long long p = pw0 + 16 * b + i16;
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const int co = co0 + 16 * a + 4 * g;
+        const bool first = co < d.split;
+        const int acc_in = first ? d.accum : d.accum2;
+        old[b][a] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p < P && acc_in)
+          old[b][a] = first ? *reinterpret_cast<const float4*>((const float*)d.out + p * d.split + co)
+                            : *reinterpret_cast<const float4*>((const float*)d.out2 + p * c2 + (co - d.split));
+      }
+    }
+  }
   for (int c = 0; c < nchunks; ++c) {
     uint4 xn[NB];
     if (c + 1 < nchunks) {
@@ -184,13 +223,25 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
         const int co = co0 + 16 * a + 4 * g;
-        float4* q;
-        int acc_in;
-        if (co < d.split) { q = reinterpret_cast<float4*>(o1 + p * d.split + co); acc_in = d.accum; }
-        else { q = reinterpret_cast<float4*>(o2 + p * c2 + (co - d.split)); acc_in = d.accum2; }
+        float4* q = co < d.split ? reinterpret_cast<float4*>(o1 + p * d.split + co)
+                                 : reinterpret_cast<float4*>(o2 + p * c2 + (co - d.split));
         float4 v = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
-        if (acc_in) {
-          const float4 o = *q;
+        if constexpr (GATED) {
+          // the x*s term as gate_bwd1 formed it (old + d*s, or d*s), then + W_x^T dy as the separate
+          // accumulating dgrad added it: the same fp32 operations in the same order
+          const float4 x = gxs[b][a];
+          const float sg = gsv[b];
+          float4 t;
+          if (d.accum) {
+            const float4 o = *q;
+            t = make_float4(__builtin_fmaf(x.x, sg, o.x), __builtin_fmaf(x.y, sg, o.y), __builtin_fmaf(x.z, sg, o.z),
+                            __builtin_fmaf(x.w, sg, o.w));
+          } else {
+            t = make_float4(x.x * sg, x.y * sg, x.z * sg, x.w * sg);
+          }
+          v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+        } else if (rmw && (co < d.split ? d.accum : d.accum2)) {
+          const float4 o = old[b][a];
           v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
         }
         *q = v;
@@ -397,6 +448,7 @@ bool pw_conv_ok(const unet_conv_desc* d) {
   if (d->dtype != UNET_BF16 || d->ksize != 1 || d->nsrc != 1 || !pw_src_ok(d->src[0], d->Cin)) return false;
   if (d->Cin % 32 || d->Cout % 16 || d->Cin > 256 || P < 32768) return false;
   if (d->out_mode == UNET_OUT_F32) { if (d->split % 4) return false; }
+  else if (d->out_mode == UNET_OUT_F32_GATED) { if (d->split != d->Cout) return false; }
   else if (d->out_mode != UNET_OUT_Y) return false;
   return (double)P * d->Cin * 2 < (double)PW_OOB;
 }
@@ -416,7 +468,10 @@ template <int NA, int NB>
 static int launch_pw(const unet_conv_desc* d, hipStream_t st) {
   const long long P = (long long)d->N * d->H * d->W;
   dim3 grid(cdiv(P, 64 * NB), d->Cout / (16 * NA));
-  hipLaunchKernelGGL((pw_conv_kernel<NA, NB>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+  if (d->out_mode == UNET_OUT_F32_GATED)
+    hipLaunchKernelGGL((pw_conv_kernel<NA, NB, true>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+  else
+    hipLaunchKernelGGL((pw_conv_kernel<NA, NB>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
   return check_launch("pw_conv");
 }
 

@@ -16,7 +16,7 @@ _LIB_PATH = Path(os.environ.get("UNET_HIP_LIB", Path(__file__).resolve().parent 
 
 F32, BF16, F16 = 0, 1, 2
 SRC_PLAIN, SRC_ACT, SRC_POOL_ACT, SRC_UP_ACT, SRC_NCHW_F32, SRC_UP_PLAIN = range(6)
-OUT_Y, OUT_F32, OUT_POOL_BWD, OUT_SHUFFLE2 = range(4)
+OUT_Y, OUT_F32, OUT_POOL_BWD, OUT_SHUFFLE2, OUT_F32_GATED = range(5)
 
 c_int, c_ll, c_float, c_vp, c_size = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 

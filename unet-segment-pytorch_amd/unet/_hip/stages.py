@@ -8,6 +8,7 @@ are folded into the consuming conv's tile loader through `unet_src` descriptors.
 
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -185,6 +186,16 @@ class ConvBN:
                 part = f32(2, rows, self.cin, device=dev)
                 d.bnb_stats = part.data_ptr()
                 dgrad["bnb_part"] = (part, rows)
+        elif dgrad["mode"] == "f32_gated":
+            # the attention gate's W_x input gradient plus the x*s term: out (+)= s * d(x*s) + W_x^T dy
+            d.out_mode = L.OUT_F32_GATED
+            d.out = dgrad["out"].data_ptr()
+            d.accum = int(dgrad.get("accum", 0))
+            d.split = self.cin
+            ps = L.Src()
+            ps.kind, ps.C, ps.H, ps.W = L.SRC_PLAIN, self.cin, H, W
+            ps.data, ps.gate_p, ps.gate_ab = vp(dgrad["dxs"]), vp(dgrad["gate_p"]), vp(dgrad["gate_ab"])
+            d.pool_src = ps
         elif dgrad["mode"] == "pool":
             d.out_mode = L.OUT_POOL_BWD
             d.out = dgrad["out"].data_ptr()
@@ -317,8 +328,11 @@ class GateStage:
         x = self.x
         dev = x.data.device
         P, Cx, Ci = x.pixels, x.C, self.ci
-        # (1) through x*s and the sigmoid; psi-BN backward sums
-        dx, dx_acc = x.grad_target()
+        # (1) through x*s and the sigmoid; psi-BN backward sums.  Where the bf16 1x1 kernel serves the W_x
+        # dgrad, the x*s term of dx is added by that dgrad's epilogue (one write of dx instead of a write
+        # here plus a read-modify-write there)
+        fuse = self._wx_gated_ok(prec, x)
+        dx, dx_acc = (None, 0) if fuse else x.grad_target()
         dq = f32(P, device=dev)
         rows1 = L.load().unet_gate_psi_rows(P)
         part1 = f32(2, rows1, device=dev)
@@ -358,7 +372,24 @@ class GateStage:
         self.cg.conv_backward(prec, dgw, self.gw_src, grads,
                               {"mode": "f32", "out": d_gup, "accum": d_gup_accum})
         dx2, acc2 = x.grad_target()
-        self.cx.conv_backward(prec, dxw, [x.src()], grads, {"mode": "f32", "out": dx2, "accum": acc2})
+        if fuse:
+            self.cx.conv_backward(prec, dxw, [x.src()], grads, {"mode": "f32_gated", "out": dx2, "accum": acc2,
+                                                                "dxs": d_xs, "gate_p": self.p,
+                                                                "gate_ab": self.psi_ab})
+        else:
+            self.cx.conv_backward(prec, dxw, [x.src()], grads, {"mode": "f32", "out": dx2, "accum": acc2})
+
+    def _wx_gated_ok(self, prec, x: Act) -> bool:
+        """Whether the W_x dgrad (Ci -> Cx 1x1) runs on the kernel that serves UNET_OUT_F32_GATED."""
+        if prec.code != L.BF16 or os.environ.get("UNET_NO_GATE_FUSE"):   # (env: A/B measurement switch)
+            return False
+        d = L.ConvDesc()
+        d.dtype, d.N, d.H, d.W, d.Cin, d.Cout, d.ksize, d.nsrc = prec.code, x.N, x.H, x.W, self.ci, x.C, 1, 1
+        s = L.Src()
+        s.kind, s.C, s.H, s.W = L.SRC_PLAIN, self.ci, x.H, x.W
+        d.src[0] = s
+        d.out_mode, d.split = L.OUT_F32_GATED, x.C
+        return conv_kernel_name(d).startswith("pw_conv_kernel")
 
 
 # ------------------------------------------------------------------------------------------------
@@ -542,6 +573,7 @@ class DownStage:
         x = self.x
         cv = x.C // 8
         if self.code is not None and x.bn_owned and x.C % 8 == 0 and cv <= 256 and cv & (cv - 1) == 0 \
+                and not os.environ.get("UNET_NO_POOL_FOLD") \
                 and x.pixels < 2 ** 31 and x.pool_grad is None and (x.grad is None or x.grad.dtype == torch.float32):
             # the dgrad is written at the pooled resolution (plain fp32 stores); the producer's BatchNorm
             # backward routes it through the argmax codes while it reads the other consumers' gradient
