@@ -66,18 +66,21 @@ __global__ void upsample_bwd4_kernel(long long N, int C, int Hs, int Ws, int up_
 // columns, true for every x2-or-less upsample): the 8 row and 8 column weights (0 outside
 // the window, the padded frame or the source support) are computed once per element instead of inside
 // the 2-D loop, and only the nonzero taps issue loads
+// (I: element index type, unsigned when N*Hs*Ws*C/4 < 2^31 — 32-bit divisions, as materialize_fast_kernel)
+template <typename I = unsigned>
 __global__ __launch_bounds__(256) void upsample_bwd4w_kernel(long long N, int C, int Hs, int Ws, int up_h, int up_w,
                                                              int pt, int pl, int Hp, int Wp, float sh, float sw,
                                                              const float* dup, float* dx, int accum) {
   const int C4 = C / 4;
-  const long long total = N * Hs * (long long)Ws * C4;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const int c4 = e % C4;
-    long long t = e / C4;
-    const int j = t % Ws;
-    t /= Ws;
-    const int i = t % Hs;
-    const long long n = t / Hs;
+  const I total = (I)(N * Hs * (long long)Ws * C4);
+  for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (I)gridDim.x * blockDim.x) {
+    I t = e / (I)C4;
+    const int c4 = (int)(e - t * (I)C4);
+    I t2 = t / (I)Ws;
+    const int j = (int)(t - t2 * (I)Ws);
+    t = t2 / (I)Hs;
+    const int i = (int)(t2 - t * (I)Hs);
+    const long long n = (long long)t;
     // u contributes to row i only if floor(sh*u) in {i-1, i}: u in [(i-1)/sh, (i+1)/sh] (+-1 guard)
     const int ulo = max(0, (int)ceilf((float)(i - 1) / sh) - 1), uhi = min(up_h - 1, (int)floorf((float)(i + 1) / sh) + 1);
     const int vlo = max(0, (int)ceilf((float)(j - 1) / sw) - 1), vhi = min(up_w - 1, (int)floorf((float)(j + 1) / sw) + 1);
@@ -586,51 +589,58 @@ struct MatDesc {
   int Cin;
 };
 
-template <typename T, int RAW>
+// I: the element index type — unsigned (32-bit division: ~10 VALU instead of a ~100-instruction 64-bit
+// division sequence, of which there are four per element) whenever N*H*W*CV < 2^31 (host-chosen)
+template <typename T, int RAW, typename I = unsigned>
 __global__ void materialize_fast_kernel(const MatDesc d, long long N, int H, int W, T* out) {
   constexpr int VEC = Vec<T>::N;
   const int C = d.src[0].C;
   const int CV = C / VEC;
-  const long long total = N * H * (long long)W * CV;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  const int cv = (int)(e % CV);
+  const int cvs = __builtin_ctz(CV);   // CV is a power of two (host-checked)
+  const I total = (I)(N * H * (long long)W * CV);
+  const I stride = (I)gridDim.x * blockDim.x;
+  I e = (I)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = (int)(e & (CV - 1));
   SrcView sv;
   float sc[VEC], sf[VEC];
   make_view<T>(d, cv * VEC, sv, sc, sf);
   for (; e < total; e += stride) {
-    const long long px = e / CV;
-    const int x = (int)(px % W);
-    const long long t = px / W;
-    const int y = (int)(t % H);
-    const int n = (int)(t / H);
+    const I px = e >> cvs;
+    const I t = px / (I)W;
+    const int x = (int)(px - t * (I)W);
+    const I t2 = t / (I)H;
+    const int y = (int)(t - t2 * (I)H);
+    const int n = (int)t2;
     Item<RAW> it;
     item_issue<T, RAW>(sv, H, W, n, y, x, 1, it);
     float v[VEC];
     item_finish<T, RAW>(d, sv, sc, sf, n, y, x, cv * VEC, it, v);
-    store_vec<T>(out + px * C + cv * VEC, v);
+    store_vec<T>(out + (size_t)px * C + cv * VEC, v);
   }
 }
 
 // MaxPool2d(2) of relu?(scale*y + shift) with argmax codes; one thread per pooled channel vector
-template <typename T>
+// (I as materialize_fast_kernel)
+template <typename T, typename I = unsigned>
 __global__ void materialize_pool_kernel(const unet_src s, long long N, int H, int W, T* out, uint8_t* code) {
   constexpr int VEC = Vec<T>::N;
   const int C = s.C, CV = C / VEC;
-  const long long total = N * H * (long long)W * CV;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  const int cv = (int)(e % CV);
+  const int cvs = __builtin_ctz(CV);
+  const I total = (I)(N * H * (long long)W * CV);
+  const I stride = (I)gridDim.x * blockDim.x;
+  I e = (I)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = (int)(e & (CV - 1));
   float sc[VEC], sf[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) { sc[j] = s.scale[cv * VEC + j]; sf[j] = s.shift[cv * VEC + j]; }
   const float lo = s.relu ? 0.f : -INFINITY;
   for (; e < total; e += stride) {
-    const long long px = e / CV;
-    const int x = (int)(px % W);
-    const long long t = px / W;
-    const int y = (int)(t % H);
-    const long long n = t / H;
+    const I px = e >> cvs;
+    const I t = px / (I)W;
+    const int x = (int)(px - t * (I)W);
+    const I t2 = t / (I)H;
+    const int y = (int)(t - t2 * (I)H);
+    const long long n = (long long)t2;
     float best[VEC];
     int arg[VEC];
 #pragma unroll
@@ -643,16 +653,16 @@ __global__ void materialize_pool_kernel(const unet_src s, long long N, int H, in
         if (q == 0 || a > best[j] || a != a) { best[j] = a; arg[j] = q; }
       }
     }
-    store_vec<T>(out + px * C + cv * VEC, best);
+    store_vec<T>(out + (size_t)px * C + cv * VEC, best);
     unsigned lo4 = 0, hi4 = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) lo4 |= (unsigned)arg[j] << (8 * j);
     if constexpr (VEC == 8) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) hi4 |= (unsigned)arg[4 + j] << (8 * j);
-      *reinterpret_cast<uint2*>(code + px * C + cv * VEC) = make_uint2(lo4, hi4);
+      *reinterpret_cast<uint2*>(code + (size_t)px * C + cv * VEC) = make_uint2(lo4, hi4);
     } else {
-      *reinterpret_cast<unsigned*>(code + px * C + cv * VEC) = lo4;
+      *reinterpret_cast<unsigned*>(code + (size_t)px * C + cv * VEC) = lo4;
     }
   }
 }
@@ -669,8 +679,12 @@ int unet_upsample_bwd(long long N, int C, int Hs, int Ws, int up_h, int up_w, in
   // widest destination window of upsample_bwd4w: floor(2/scale) + 3 taps (scale 0: the whole map)
   auto span = [](float sc, int up) { return sc > 0.f ? (int)floorf(2.f / sc) + 3 : up + 8; };
   if (C % 4 == 0 && span(sh, up_h) <= 8 && span(sw, up_w) <= 8) {
-    hipLaunchKernelGGL(upsample_bwd4w_kernel, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream, N, C, Hs,
-                       Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
+    if (total / 4 < (1LL << 31))
+      hipLaunchKernelGGL(upsample_bwd4w_kernel<unsigned>, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream,
+                         N, C, Hs, Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
+    else
+      hipLaunchKernelGGL(upsample_bwd4w_kernel<unsigned long long>, dim3(grid_for(total / 4)), dim3(256), 0,
+                         (hipStream_t)stream, N, C, Hs, Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
     return check_launch("upsample_bwd");
   }
   if (C % 4 == 0) {
@@ -855,16 +869,18 @@ int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, 
     md.Cin = src->C;
     const int raw = (src->kind == UNET_SRC_POOL_ACT || src->kind == UNET_SRC_UP_ACT) ? 4 : 1;
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == UNET_BF16) {
-      if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<bf16, 4>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (bf16*)out);
-      else hipLaunchKernelGGL((materialize_fast_kernel<bf16, 1>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (bf16*)out);
-    } else if (dtype == UNET_F16) {
-      if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<f16, 4>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (f16*)out);
-      else hipLaunchKernelGGL((materialize_fast_kernel<f16, 1>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (f16*)out);
-    } else {
-      if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<float, 4>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (float*)out);
-      else hipLaunchKernelGGL((materialize_fast_kernel<float, 1>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (float*)out);
-    }
+    const bool i32 = total < (1LL << 31);
+#define UNET_MAT_LAUNCH(TT)                                                                                        \
+  do {                                                                                                           \
+    if (raw == 4 && i32) hipLaunchKernelGGL((materialize_fast_kernel<TT, 4, unsigned>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (TT*)out); \
+    else if (raw == 4) hipLaunchKernelGGL((materialize_fast_kernel<TT, 4, unsigned long long>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (TT*)out); \
+    else if (i32) hipLaunchKernelGGL((materialize_fast_kernel<TT, 1, unsigned>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (TT*)out); \
+    else hipLaunchKernelGGL((materialize_fast_kernel<TT, 1, unsigned long long>), dim3((int)b), dim3(256), 0, st, md, N, H, W, (TT*)out); \
+  } while (0)
+    if (dtype == UNET_BF16) UNET_MAT_LAUNCH(bf16);
+    else if (dtype == UNET_F16) UNET_MAT_LAUNCH(f16);
+    else UNET_MAT_LAUNCH(float);
+#undef UNET_MAT_LAUNCH
     return check_launch("materialize");
   }
   if (dtype == UNET_F16)
@@ -892,12 +908,19 @@ int unet_materialize_pool(int dtype, const unet_src* src, long long N, int H, in
   long long b = (total + 255) / 256;
   if (b > 16384) b = 16384;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == UNET_F16)
-    hipLaunchKernelGGL(materialize_pool_kernel<f16>, dim3((int)b), dim3(256), 0, st, *src, N, H, W, (f16*)out, code);
+  const bool i32 = total < (1LL << 31);
+  if (dtype == UNET_F16 && i32)
+    hipLaunchKernelGGL((materialize_pool_kernel<f16, unsigned>), dim3((int)b), dim3(256), 0, st, *src, N, H, W, (f16*)out, code);
+  else if (dtype == UNET_F16)
+    hipLaunchKernelGGL((materialize_pool_kernel<f16, unsigned long long>), dim3((int)b), dim3(256), 0, st, *src, N, H, W, (f16*)out, code);
+  else if (dtype == UNET_BF16 && i32)
+    hipLaunchKernelGGL((materialize_pool_kernel<bf16, unsigned>), dim3((int)b), dim3(256), 0, st, *src, N, H, W, (bf16*)out, code);
   else if (dtype == UNET_BF16)
-    hipLaunchKernelGGL(materialize_pool_kernel<bf16>, dim3((int)b), dim3(256), 0, st, *src, N, H, W, (bf16*)out, code);
+    hipLaunchKernelGGL((materialize_pool_kernel<bf16, unsigned long long>), dim3((int)b), dim3(256), 0, st, *src, N, H, W, (bf16*)out, code);
+  else if (i32)
+    hipLaunchKernelGGL((materialize_pool_kernel<float, unsigned>), dim3((int)b), dim3(256), 0, st, *src, N, H, W, (float*)out, code);
   else
-    hipLaunchKernelGGL(materialize_pool_kernel<float>, dim3((int)b), dim3(256), 0, st, *src, N, H, W, (float*)out, code);
+    hipLaunchKernelGGL((materialize_pool_kernel<float, unsigned long long>), dim3((int)b), dim3(256), 0, st, *src, N, H, W, (float*)out, code);
   return check_launch("materialize_pool");
 }
 
