@@ -17,7 +17,7 @@ timeout -k 10 200 python -u tools/layerprof.py > $O/layerprof.txt 2>&1 || { echo
 i=0
 for set in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex 'conv3_kernel' --output-format csv -d $O/pmc$i -o pmc -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $O/pmc$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex 'conv3_kernel' --output-format csv -d $O/pmc$i -o pmc -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-fp32-line > $O/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $O/pmc$i.log; exit 1; }
   python tools/pmcsum.py $O/pmc$i conv3_kernel
 done
 echo done
