@@ -310,12 +310,13 @@ def _pw_var(L, d):
     return buf.value.decode()
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("shape", PW_SHAPES)
 @pytest.mark.parametrize("gate", [False, True])
-def test_pw_fwd_stats(shape, gate):
+def test_pw_fwd_stats(shape, gate, prec):
     L = _lib()
     N, H, W, cin, cout = shape
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(5)
     y = _rand(N, H, W, cin, dt=dt)
     ab = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2])
@@ -329,7 +330,7 @@ def test_pw_fwd_stats(shape, gate):
     w = (torch.randn(cout, cin, 1, 1, device="cuda") * 0.1).to(dt).float()
     out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
     st = torch.zeros(2, cout, 8192, device="cuda")
-    d = _conv("bf16", [src], N, H, W, cin, w, 1, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
+    d = _conv(prec, [src], N, H, W, cin, w, 1, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
     assert _pw_var(L, d).startswith("pw_conv_kernel"), _pw_var(L, d)
     ref = F.conv2d(x.to(dt).float().permute(0, 3, 1, 2), w).permute(0, 2, 3, 1)
     assert (out.float() - ref).abs().max() <= 2e-2 * (1 + ref.abs().max())
@@ -340,11 +341,12 @@ def test_pw_fwd_stats(shape, gate):
     assert torch.allclose(sums[1], (r * r).sum(0), rtol=1e-3, atol=1e-1)
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("shape", PW_SHAPES)
-def test_pw_dgrad_split_accum(shape):
+def test_pw_dgrad_split_accum(shape, prec):
     L = _lib()
     N, H, W, cin, cout = shape     # forward 1x1 conv cin -> cout; dgrad dy[cout] -> dx[cin]
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(6)
     dy = _rand(N, H, W, cout, dt=dt)
     w = (torch.randn(cout, cin, 1, 1, device="cuda") * 0.1).to(dt).float()
@@ -354,7 +356,7 @@ def test_pw_dgrad_split_accum(shape):
     split = cin // 2
     o1 = torch.full((N, H, W, split), 1.0, device="cuda")
     o2 = torch.full((N, H, W, cin - split), float("nan"), device="cuda")
-    d = _conv("bf16", [src], N, H, W, cout, w, 1, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
+    d = _conv(prec, [src], N, H, W, cout, w, 1, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
               split=split, accum=1, accum2=0)
     if cout % 32 == 0:
         assert _pw_var(L, d).startswith("pw_conv_kernel"), _pw_var(L, d)
@@ -362,12 +364,13 @@ def test_pw_dgrad_split_accum(shape):
     assert (got - ref).abs().max() <= 2e-2 * (1 + ref.abs().max())
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("shape", PW_SHAPES)
 @pytest.mark.parametrize("gate", [False, True])
-def test_pw_wgrad(shape, gate):
+def test_pw_wgrad(shape, gate, prec):
     L, R = _lib(), _rt()
     N, H, W, cin, cout = shape
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(7)
     dy = _rand(N, H, W, cout, dt=dt)
     ab = torch.stack([torch.randn(cin, device="cuda"), torch.randn(cin, device="cuda") * 0.2])
@@ -382,7 +385,7 @@ def test_pw_wgrad(shape, gate):
     x = x.to(dt).float().permute(0, 3, 1, 2)
     ref = torch.nn.grad.conv2d_weight(x, (cout, cin, 1, 1), dy.float().permute(0, 3, 1, 2))
     wd = L.WgradDesc()
-    wd.dtype = R.BF16.code
+    wd.dtype = R._PRECISIONS[prec].code
     wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = N, H, W, cin, cout, 1, 1
     wd.src[0] = src
     wd.dy = dy.data_ptr()
@@ -841,13 +844,14 @@ def test_bn_backward_pooled_gradient(prec, shape, with_da):
 @pytest.mark.parametrize("shape", [(4, 128, 128, 64, 32), (4, 181, 183, 64, 64), (4, 200, 170, 32, 64)],
                          ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("accum", [0, 1])
-def test_pw_dgrad_gated(shape, accum):
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_pw_dgrad_gated(shape, accum, prec):
     """UNET_OUT_F32_GATED: the attention gate's W_x input gradient with the x*s term fused in,
     out (+)= sigmoid(p*a+b) * d(x*s) + W_x^T dy (layers.py:171-192), against torch; the pass-1 kernel then
     writes no dx (unet_gate_bwd1 with dx = NULL)."""
     L, R = _lib(), _rt()
     N, H, W, cin, cout = shape     # forward 1x1 conv cin (= Cx) -> cout (= Ci); dgrad dy[cout] -> dx[cin]
-    dt = torch.bfloat16
+    dt = DT[prec]
     torch.manual_seed(7)
     dy = _rand(N, H, W, cout, dt=dt)
     w = (torch.randn(cout, cin, 1, 1, device="cuda") * 0.1).to(dt).float()
@@ -861,7 +865,7 @@ def test_pw_dgrad_gated(shape, accum):
     ps = L.Src()
     ps.kind, ps.C, ps.H, ps.W = L.SRC_PLAIN, cin, H, W
     ps.data, ps.gate_p, ps.gate_ab = dxs.data_ptr(), p.data_ptr(), ab.data_ptr()
-    d = _conv("bf16", [src], N, H, W, cout, w, 1, L.OUT_F32_GATED, transpose=True, out=out.data_ptr(),
+    d = _conv(prec, [src], N, H, W, cout, w, 1, L.OUT_F32_GATED, transpose=True, out=out.data_ptr(),
               split=cin, accum=accum, pool_src=ps)
     assert _pw_var(L, d).startswith("pw_conv_kernel"), _pw_var(L, d)
     s = torch.sigmoid(p * ab[0] + ab[1]).unsqueeze(-1)
@@ -880,9 +884,9 @@ def test_pw_dgrad_gated(shape, accum):
     part1, part2 = torch.empty(2, rows, device="cuda"), torch.empty(2, rows, device="cuda")
     dx = torch.empty(N, H, W, cin, device="cuda")
     vp = R_.vp
-    L.call("unet_gate_bwd1", L.BF16, P, cin, vp(dxs), vp(y), vp(sc), vp(sf), 1, vp(p), vp(ab), vp(pm), vp(pi), vp(dx),
+    L.call("unet_gate_bwd1", R_._PRECISIONS[prec].code, P, cin, vp(dxs), vp(y), vp(sc), vp(sf), 1, vp(p), vp(ab), vp(pm), vp(pi), vp(dx),
            0, vp(dq1), vp(part1), R_.stream())
-    L.call("unet_gate_bwd1", L.BF16, P, cin, vp(dxs), vp(y), vp(sc), vp(sf), 1, vp(p), vp(ab), vp(pm), vp(pi), None,
+    L.call("unet_gate_bwd1", R_._PRECISIONS[prec].code, P, cin, vp(dxs), vp(y), vp(sc), vp(sf), 1, vp(p), vp(ab), vp(pm), vp(pi), None,
            0, vp(dq2), vp(part2), R_.stream())
     torch.cuda.synchronize()
     assert torch.equal(dq1, dq2) and torch.equal(part1, part2)

@@ -15,7 +15,7 @@
 //    (double-buffered, one barrier per tile) and read with the CDNA4 transposed read
 //    ds_read_b64_tr_b16 so the pixel index runs along K; split-K partial slabs are summed in a fixed
 //    order by wgrad_reduce2 (deterministic).
-#include "common.h"
+#include "conv_common.h"
 
 namespace unet {
 
@@ -28,30 +28,21 @@ __device__ __forceinline__ pw_rsrc_t pw_rsrc(const void* p, unsigned bytes) {
 __device__ __forceinline__ uint4 pw_ld(pw_rsrc_t r, unsigned voff, unsigned soff) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
-__device__ __forceinline__ unsigned pw_pack2(float a, float b) {
-  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-  const bf16x2 p = {(__bf16)a, (__bf16)b};
-  return __builtin_bit_cast(unsigned, p);
-}
-
-// 8 bf16 channels (one lane's 16-byte vector) through the source transform
-__device__ __forceinline__ bf16x8 pw_act(uint4 q, bool act, const float* sc, const float* sf, float lo, float gmul) {
-  if (!act && gmul == 1.f) return __builtin_bit_cast(bf16x8, q);
-  const unsigned u[4] = {q.x, q.y, q.z, q.w};
+// 8 channels (one lane's 16-byte vector of the 16-bit operand type T) through the source transform
+template <typename T>
+__device__ __forceinline__ typename Mma<T>::frag pw_act(uint4 q, bool act, const float* sc, const float* sf, float lo,
+                                                        float gmul) {
+  typedef typename Mma<T>::frag F;
+  if (!act && gmul == 1.f) return __builtin_bit_cast(F, q);
   float v[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(u[i] << 16);
-    v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
-  }
+  unpack8_16<T>(q, v);
   if (act) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] *= gmul;
-  const uint4 r = make_uint4(pw_pack2(v[0], v[1]), pw_pack2(v[2], v[3]), pw_pack2(v[4], v[5]), pw_pack2(v[6], v[7]));
-  return __builtin_bit_cast(bf16x8, r);
+  return __builtin_bit_cast(F, pack8_16<T>(v));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -59,8 +50,9 @@ __device__ __forceinline__ bf16x8 pw_act(uint4 q, bool act, const float* sc, con
 // ------------------------------------------------------------------------------------------------
 // GATED (UNET_OUT_F32_GATED): the attention gate's W_x input gradient, with the x*s term of the same
 // gradient added here instead of by gate_bwd1: d(x*s) and s = sigmoid(psi) are loaded ahead of the MFMAs
-template <int NA, int NB, bool GATED = false>
+template <typename T, int NA, int NB, bool GATED = false>
 __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, long long P, int nchunks) {
+  typedef typename Mma<T>::frag F;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i16 = lane & 15, g = lane >> 4;
   const long long pw0 = ((long long)blockIdx.x * 4 + wave) * (16 * NB);
@@ -152,14 +144,14 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
       sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
       sf[0] = f0.x; sf[1] = f0.y; sf[2] = f0.z; sf[3] = f0.w; sf[4] = f1.x; sf[5] = f1.y; sf[6] = f1.z; sf[7] = f1.w;
     }
-    bf16x8 xb[NB];
+    F xb[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) xb[b] = pw_act(xq[b], act, sc, sf, lo, gm[b]);
+    for (int b = 0; b < NB; ++b) xb[b] = pw_act<T>(xq[b], act, sc, sf, lo, gm[b]);
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-      const bf16x8 wa = __builtin_bit_cast(bf16x8, wq[a]);
+      const F wa = __builtin_bit_cast(F, wq[a]);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xb[b], acc[a][b], 0, 0, 0);
+      for (int b = 0; b < NB; ++b) acc[a][b] = Mma<T>::mma(wa, xb[b], acc[a][b]);
     }
     if (c + 1 < nchunks) {
 #pragma unroll
@@ -169,7 +161,7 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
 
   // epilogue: acc[a][b][r] = out[px = pw0 + 16b + i16][co = co0 + 16a + 4g + r]
   if (d.out_mode == UNET_OUT_Y) {
-    bf16* y = (bf16*)d.out;
+    T* y = (T*)d.out;
     float sm[NA][4], sq[NA][4];
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -183,7 +175,7 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
         const int co = co0 + 16 * a + 4 * g;
         if (p < P) {
           const f32x4 v = acc[a][b];
-          *reinterpret_cast<uint2*>(y + p * d.Cout + co) = make_uint2(pw_pack2(v[0], v[1]), pw_pack2(v[2], v[3]));
+          *reinterpret_cast<uint2*>(y + p * d.Cout + co) = make_uint2(pack2_16<T>(v[0], v[1]), pack2_16<T>(v[2], v[3]));
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {  // pixels past P accumulated exact zeros
@@ -256,16 +248,18 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
 // ------------------------------------------------------------------------------------------------
 constexpr int PW_KP = 64;  // pixels per staged tile
 
-__device__ __forceinline__ bf16x8 pw_tr8(const bf16* r0, const bf16* r1) {
+template <typename T>
+__device__ __forceinline__ typename Mma<T>::frag pw_tr8(const T* r0, const T* r1) {
   const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r0));
   const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(r1));
   typedef __attribute__((ext_vector_type(8))) short i16x8;
   const i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, r);
+  return __builtin_bit_cast(typename Mma<T>::frag, r);
 }
 
-template <int MA, int MB>
+template <typename T, int MA, int MB>
 __global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, long long P, int per_split, float* ws) {
+  typedef typename Mma<T>::frag F;
   constexpr int BCO = 16 * MA, BCI = 64 * MB;
   // LDS row strides: odd multiples of 32 B (see wgrad2.hip) so the tr reads are conflict-free
   constexpr int RSD = BCO + (BCO % 32 == 0 ? 16 : 32 - BCO % 32 + 16);
@@ -274,7 +268,7 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, 
   constexpr int NVD = BCO / 8, NVX = BCI / 8;              // 16-byte vectors per pixel row
   constexpr int ID = (PW_KP * NVD + 255) / 256, IX = (PW_KP * NVX + 255) / 256;
   constexpr int BUF = PW_KP * (RSD + RSX);
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * BUF];
+  __shared__ __attribute__((aligned(16))) T lds[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int co0 = blockIdx.z * BCO, ci0 = blockIdx.y * BCI;
@@ -320,14 +314,14 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, 
       qd[k] = pw_ld(dr, ok ? (unsigned)p * dpix + (unsigned)cd * 2u : PW_OOB, 0);
     }
   };
-  auto finish = [&](bf16* buf) {
-    bf16* bd = buf;
-    bf16* bx = buf + PW_KP * RSD;
+  auto finish = [&](T* buf) {
+    T* bd = buf;
+    T* bx = buf + PW_KP * RSD;
 #pragma unroll
     for (int k = 0; k < IX; ++k) {
       const int pr = (tid + 256 * k) / NVX;
       if (pr < PW_KP)
-        *reinterpret_cast<bf16x8*>(bx + pr * RSX + vx * 8) = pw_act(qx[k], act, sc, sf, lo, gx[k]);
+        *reinterpret_cast<F*>(bx + pr * RSX + vx * 8) = pw_act<T>(qx[k], act, sc, sf, lo, gx[k]);
     }
 #pragma unroll
     for (int k = 0; k < ID; ++k) {
@@ -353,22 +347,22 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, 
   const int sw = (g & 1) * 4;
   for (long long t = t_begin; t < t_end; ++t) {
     const int cur = (int)((t - t_begin) & 1);
-    const bf16* bd = lds + cur * BUF;
-    const bf16* bx = bd + PW_KP * RSD;
+    const T* bd = lds + cur * BUF;
+    const T* bx = bd + PW_KP * RSD;
     const bool has_next = t + 1 < t_end;
     if (has_next) issue(t + 1);
 #pragma unroll
     for (int k0 = 0; k0 < PW_KP; k0 += 32) {
       const int r0 = k0 + 8 * g + q + sw, r1 = k0 + 8 * g + q + 4 - sw;
-      bf16x8 av[MA];
+      F av[MA];
 #pragma unroll
-      for (int a = 0; a < MA; ++a) av[a] = pw_tr8(bd + r0 * RSD + 16 * a + p4, bd + r1 * RSD + 16 * a + p4);
+      for (int a = 0; a < MA; ++a) av[a] = pw_tr8<T>(bd + r0 * RSD + 16 * a + p4, bd + r1 * RSD + 16 * a + p4);
 #pragma unroll
       for (int b = 0; b < MB; ++b) {
         const int col = 16 * (wave * MB + b) + p4;
-        const bf16x8 bv = pw_tr8(bx + r0 * RSX + col, bx + r1 * RSX + col);
+        const F bv = pw_tr8<T>(bx + r0 * RSX + col, bx + r1 * RSX + col);
 #pragma unroll
-        for (int a = 0; a < MA; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv, acc[a][b], 0, 0, 0);
+        for (int a = 0; a < MA; ++a) acc[a][b] = Mma<T>::mma(av[a], bv, acc[a][b]);
       }
     }
     if (has_next) finish(lds + (cur ^ 1) * BUF);
@@ -445,7 +439,9 @@ static bool pw_src_ok(const unet_src& s, int C) {
 // tiled conv2 / wgrad2 paths, which re-use weights across more pixels per workgroup
 bool pw_conv_ok(const unet_conv_desc* d) {
   const long long P = (long long)d->N * d->H * d->W;
-  if (d->dtype != UNET_BF16 || d->ksize != 1 || d->nsrc != 1 || !pw_src_ok(d->src[0], d->Cin)) return false;
+  if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 1 || d->nsrc != 1 ||
+      !pw_src_ok(d->src[0], d->Cin))
+    return false;
   if (d->Cin % 32 || d->Cout % 16 || d->Cin > 256 || P < 32768) return false;
   if (d->out_mode == UNET_OUT_F32) { if (d->split % 4) return false; }
   else if (d->out_mode == UNET_OUT_F32_GATED) { if (d->split != d->Cout) return false; }
@@ -464,29 +460,35 @@ int pw_conv_rows(const unet_conv_desc* d) {
   return cdiv((long long)d->N * d->H * d->W, 64 * nb);
 }
 
-template <int NA, int NB>
+template <typename T, int NA, int NB>
 static int launch_pw(const unet_conv_desc* d, hipStream_t st) {
   const long long P = (long long)d->N * d->H * d->W;
   dim3 grid(cdiv(P, 64 * NB), d->Cout / (16 * NA));
   if (d->out_mode == UNET_OUT_F32_GATED)
-    hipLaunchKernelGGL((pw_conv_kernel<NA, NB, true>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, true>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
   else
-    hipLaunchKernelGGL((pw_conv_kernel<NA, NB>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
   return check_launch("pw_conv");
 }
 
-int pw_conv(const unet_conv_desc* d, hipStream_t st) {
+template <typename T>
+static int pw_conv_t(const unet_conv_desc* d, hipStream_t st) {
   int na, nb;
   pw_conv_geom(d, na, nb);
-  if (na == 4) return launch_pw<4, 4>(d, st);
-  if (na == 2) return launch_pw<2, 4>(d, st);
-  return launch_pw<1, 4>(d, st);
+  if (na == 4) return launch_pw<T, 4, 4>(d, st);
+  if (na == 2) return launch_pw<T, 2, 4>(d, st);
+  return launch_pw<T, 1, 4>(d, st);
+}
+
+int pw_conv(const unet_conv_desc* d, hipStream_t st) {
+  return d->dtype == UNET_F16 ? pw_conv_t<f16>(d, st) : pw_conv_t<bf16>(d, st);
 }
 
 int pw_conv_variant(const unet_conv_desc* d, char* buf, int len) {
   int na, nb;
   pw_conv_geom(d, na, nb);
-  snprintf(buf, len, "pw_conv_kernel<%d,%d>", na, nb);
+  if (d->dtype == UNET_F16) snprintf(buf, len, "pw_conv_kernel<fp16,%d,%d>", na, nb);
+  else snprintf(buf, len, "pw_conv_kernel<%d,%d>", na, nb);
   return 0;
 }
 
@@ -497,7 +499,9 @@ struct PwWPlan {
 
 bool pw_wgrad_ok(const unet_wgrad_desc* d) {
   const long long P = (long long)d->N * d->H * d->W;
-  if (d->dtype != UNET_BF16 || d->ksize != 1 || d->nsrc != 1 || !pw_src_ok(d->src[0], d->Cin)) return false;
+  if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 1 || d->nsrc != 1 ||
+      !pw_src_ok(d->src[0], d->Cin))
+    return false;
   if (d->Cin % 64 || d->Cout % 16 || P < 131072) return false;  // measured: wgrad2 wins at 128^2 x bs4
   return (double)P * d->Cin * 2 < (double)PW_OOB && (double)P * d->Cout * 2 < (double)PW_OOB;
 }
@@ -527,7 +531,10 @@ template <int MA, int MB>
 static int launch_pww(const unet_wgrad_desc* d, const PwWPlan& p, hipStream_t st) {
   const long long P = (long long)d->N * d->H * d->W;
   dim3 grid(p.splits, d->Cin / (64 * MB), d->Cout / (16 * MA));
-  hipLaunchKernelGGL((pw_wgrad_kernel<MA, MB>), grid, dim3(256), 0, st, *d, P, p.per_split, (float*)d->workspace);
+  if (d->dtype == UNET_F16)
+    hipLaunchKernelGGL((pw_wgrad_kernel<f16, MA, MB>), grid, dim3(256), 0, st, *d, P, p.per_split, (float*)d->workspace);
+  else
+    hipLaunchKernelGGL((pw_wgrad_kernel<bf16, MA, MB>), grid, dim3(256), 0, st, *d, P, p.per_split, (float*)d->workspace);
   return check_launch("pw_wgrad");
 }
 

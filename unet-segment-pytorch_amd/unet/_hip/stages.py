@@ -381,7 +381,7 @@ class GateStage:
 
     def _wx_gated_ok(self, prec, x: Act) -> bool:
         """Whether the W_x dgrad (Ci -> Cx 1x1) runs on the kernel that serves UNET_OUT_F32_GATED."""
-        if prec.code != L.BF16 or os.environ.get("UNET_NO_GATE_FUSE"):   # (env: A/B measurement switch)
+        if prec.code not in (L.BF16, L.F16) or os.environ.get("UNET_NO_GATE_FUSE"):   # (env: A/B switch)
             return False
         d = L.ConvDesc()
         d.dtype, d.N, d.H, d.W, d.Cin, d.Cout, d.ksize, d.nsrc = prec.code, x.N, x.H, x.W, self.ci, x.C, 1, 1
