@@ -102,8 +102,8 @@ def max_over_ranks(elapsed: float, device: torch.device) -> float:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="attention_unet", choices=["attention_unet", "unet"])
     ap.add_argument("--batch", type=int, default=4, help="per-GPU batch")
     ap.add_argument("--size", type=int, default=512)
