@@ -84,7 +84,10 @@ def cpu_baseline(model_kind: str, size: int, batch: int, iters: int) -> dict:
     for _ in range(iters):
         one()
     dt = time.perf_counter() - t0
+    # threads: torch's intra-op pool, which follows OMP_NUM_THREADS (16 on the GPU box: the job's share of
+    # the host); os.cpu_count() there reports the whole machine, and 256 threads on a 16-core share thrash
     return {"value": round(batch * iters / dt, 4), "unit": "img/s", "cores": torch.get_num_threads(),
+            "cores_note": "torch.get_num_threads() = the job's CPU share (OMP_NUM_THREADS); host_cpus = os.cpu_count()",
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "kind": "port",
             "sample": f"oracle/unet_oracle.py fp32 CPU, {model_kind} 1x{size}x{size}, batch {batch}, "
                       f"1 warm-up + {iters} timed fwd+DiceBCE+bwd iterations ({dt:.1f} s)"}
@@ -193,11 +196,15 @@ def main():
         step()
     elapsed, loss = timed(step, args.steps)          # the headline: no probe events inside
 
-    # the dominant kernel, timed live in a separate pass of the same steps: every 16-bit 3x3 conv launch
-    # (fwd + dgrad; all tile instantiations of conv3_kernel, prefix match), ~44 % of the step
+    # the dominant kernel family, timed live in a separate pass of the same steps: every 16-bit 3x3 conv
+    # launch (fwd + dgrad; the 32x32x16-MFMA conv4_kernel tiles on the large maps and the 16x16x32
+    # conv3_kernel tiles on the rest, prefix match)
     tn = {"bf16": "bf16", "fp16": "fp16"}.get(args.precision)
-    target = args.probe or (f"conv3_kernel<{tn},3," if tn else "conv2_kernel<fp32,3,")
-    probe.enable(target)
+    family = (f"conv3_kernel<{tn},3,", f"conv4_kernel<{tn},") if tn else ("conv2_kernel<fp32,3,",)
+    if args.probe:
+        family = (args.probe,)
+    target = "|".join(family)
+    probe.enable(family)
     timed(step, max(2, min(args.steps, 10)))
     probe.disable()
     ps = probe.summary()

@@ -31,7 +31,11 @@ enum { UNET_ERR_ARG = 1001, UNET_ERR_UNSUPPORTED = 1002 };
 
 /* How a convolution input channel range is produced from a stored tensor ("virtual activation").
  * The conv kernels apply these transforms while staging input tiles into LDS, so BN-apply, ReLU,
- * max-pool, bilinear upsample, zero-pad and the attention multiply are never materialised. */
+ * zero-pad, the concat and the attention multiply are never materialised.  The network plan does
+ * write two derived maps once per step with unet_materialize / unet_materialize_pool (the 2x2
+ * max-pooled input of each Down block and the bilinear x2 upsample of each Up block's decoder
+ * input), because a 4-corner gather inside the MFMA kernels measured slower; the POOL_ACT / UP_ACT
+ * kinds remain for standalone module calls and those materialise kernels. */
 enum {
   UNET_SRC_PLAIN = 0,    /* x[n,h,w,c] as stored                                                  */
   UNET_SRC_ACT = 1,      /* relu?(x*scale[c]+shift[c]) (train/eval BN apply + ReLU), optional gate  */
@@ -157,15 +161,20 @@ int unet_bn_finalize(const float* stats, int rows, int C, long long count, const
                      const float* beta, float* running_mean, float* running_var,
                      long long* num_batches_tracked, float momentum, float eps,
                      float* mean, float* invstd, float* scale, float* shift, void* stream);
+/* eval mode: scale/shift from the running statistics; mean / invstd (optional, may be NULL) receive
+ * running_mean and 1/sqrt(running_var + eps) for the backward of an eval-mode forward             */
 int unet_bn_eval_affine(int C, const float* gamma, const float* beta, const float* running_mean,
-                        const float* running_var, float eps, float* scale, float* shift, void* stream);
+                        const float* running_var, float eps, float* scale, float* shift, float* mean,
+                        float* invstd, void* stream);
 /* backward: g = da * [scale*y+shift > 0] (relu!=0) ; partial sums of g and g*xhat              */
 int unet_bn_bwd_reduce_rows(long long P, int C);
 /* da: gradient w.r.t. the activation, fp32 (da_dtype UNET_F32) or bf16 (UNET_BF16, with dtype UNET_BF16) */
 int unet_bn_bwd_reduce(int dtype, int da_dtype, long long P, int C, const void* da, const void* y,
                        const float* scale, const float* shift, int relu, const float* mean,
                        const float* invstd, float* partial, void* stream);
-/* -> dgamma, dbeta (fp32 [C], stored or accumulated) and coef[3][C] with dy = A*g + B*y + Cc    */
+/* -> dgamma, dbeta (fp32 [C], stored or accumulated) and coef[3][C] with dy = A*g + B*y + Cc.
+ * count = the batch-statistics pixel count; count == 0: eval mode (running statistics, which the
+ * backward treats as constants): A = gamma*invstd, B = Cc = 0                                      */
 int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
                          const float* gamma, const float* mean, const float* invstd, float* dgamma,
                          float* dbeta, int accum, float* coef, void* stream);
@@ -267,10 +276,11 @@ int unet_materialize_pool(int dtype, const unet_src* src, long long N, int H, in
                           void* stream);
 
 /* ---- segmentation metrics — SegmentationMetrics.update, metrics.py:55-84 ----------------------- */
-/* confusion[t][p] += #pixels with target t, predicted class p (argmax over the K fp32 NCHW logits,
- * or the int64 labels when logits == NULL); pixels with t == ignore_index (has_ignore != 0) or a class
- * outside [0, K) are skipped.  confusion: int64 [K][K] on the device, accumulated (never cleared).  */
-int unet_confusion_matrix(long long N, int K, long long HW, const float* logits, const int64_t* labels,
+/* confusion[t][p] += #pixels with target t, predicted class p (argmax over the C fp32 NCHW logit
+ * channels — C may differ from K, as the reference's argmax-then-count allows — or the int64 labels
+ * when logits == NULL); pixels with t == ignore_index (has_ignore != 0) or a t or p outside [0, K) are
+ * skipped (metrics.py:68-84).  confusion: int64 [K][K] on the device, accumulated (never cleared).  */
+int unet_confusion_matrix(long long N, int C, int K, long long HW, const float* logits, const int64_t* labels,
                           const int64_t* targets, long long ignore_index, int has_ignore, int64_t* confusion,
                           void* stream);
 /* compute_iou / compute_dice, metrics.py:160-231: a (K+1) x (K+1) matrix (int64, accumulated) whose

@@ -1,0 +1,266 @@
+"""Every BASELINE.json configuration at its own size, and 16-bit gates that discriminate.
+
+* C2 — plain UNet(1, 2), base 64, 4 x 1 x 512 x 512 (reference unet/models/unet.py:37-92): fp32 operand mode
+  against the CPU fp32 oracle (logits within 1e-4, argmax equal up to near-ties, confusion matrix equal,
+  loss, gradients no worse than the reference's own fp32 error), and bf16 against the fp64 oracle beside
+  PyTorch's autocast-bf16 run, with the benchmark's conv instantiations asserted.
+* C5 — AttentionUNet(3, 2), base 64, 2 x 3 x 1024 x 1024, fp16 (configs/lung_tumor.yaml:16-27): fwd + bwd
+  against the fp64 oracle beside autocast-fp16, the 1024^2 conv instantiations asserted, and a
+  torch.amp.GradScaler step (scripts/train.py:133-143 under fp16).
+* The discriminating 16-bit gate — eval-mode BatchNorm (running statistics set to one batch's statistics,
+  so no batch-statistic amplification of 16-bit rounding), full-size forward AND backward against fp64:
+  logits and all-parameter gradient rel-L2 <= 2e-2, for C2 (UNet) and C3 (AttentionUNet), bf16 and fp16.
+  In train mode the same comparison sits at ~0.5 for autocast itself (test_gpu_fullsize.py), too loose to
+  catch a wiring error; here a wrong gradient in any stage would show.
+* The BatchNorm-backward sums fused into the dgrad's y epilogue (conv3 OM_Y_BNB, unet_conv_desc.bnb_*)
+  against the separate reduction pass (UNET_NO_BNB_FUSE): forward bit-identical, BN weight / bias gradients
+  of every layer within fp32 summation-order noise, every other gradient within 16-bit rounding of the
+  recomputed dy (the two reductions sum in different orders, so the coefficients of dy = A g + B y + C
+  differ in the last fp32 bits and a few 16-bit roundings of dy flip).
+"""
+
+import os
+
+import pytest
+import torch
+
+from fullsize_common import (batch_running_stats, discs, grad_errs, hip_run, oracle_run, rel_l2, report16,
+                             seeded_init)
+
+pytestmark = pytest.mark.gpu
+
+N, S = 4, 512
+
+
+def _threads():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+
+
+def _conv_kinds(log):
+    """{instantiation name} of the 3x3 / 1x1 convs launched, split by family"""
+    names = {k for k, _ in log}
+    return names
+
+
+# ------------------------------------------------------------------------------------------------
+# C2: plain UNet, 1 x 512^2, batch 4
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def c2_ref():
+    _threads()
+    init = seeded_init("unet", 1)
+    g = torch.Generator().manual_seed(2025)
+    x = torch.rand(N, 1, S, S, generator=g) * 2 - 1
+    t = discs(N, S, S, g)
+    return {"init": init, "x": x, "t": t,
+            "cpu32": oracle_run(init, x, t, "cpu", torch.float32, kind="unet"),
+            "f64": oracle_run(init, x, t, "cuda", torch.float64, kind="unet"),
+            "ac16": oracle_run(init, x, t, "cuda", torch.float32, kind="unet", autocast=torch.bfloat16)}
+
+
+def test_c2_unet_fp32_vs_oracle(c2_ref):
+    from oracle import unet_oracle as O
+    from unet.utils.metrics import SegmentationMetrics
+    ref, c32, f64 = c2_ref, c2_ref["cpu32"], c2_ref["f64"]
+    m, out, loss, grads = hip_run(ref["init"], ref["x"], ref["t"], "fp32", kind="unet")
+    z, zr = out.double().cpu(), c32["out"]
+    e = float((z - zr).abs().max())
+    margin = (zr[:, 1] - zr[:, 0]).abs()
+    flips = z.argmax(1) != zr.argmax(1)
+    near, hard = int((flips & (margin < 1e-4)).sum()), int((flips & (margin >= 1e-4)).sum())
+    sm = SegmentationMetrics(2)
+    sm.update(out, ref["t"].cuda())
+    cm_diff = int(abs(sm.get_confusion_matrix() - O.confusion_matrix(zr.argmax(1), ref["t"]).numpy()).sum())
+    w_h, k_h, r_h = grad_errs(grads, f64["grads"])
+    w_c, k_c, r_c = grad_errs(c32["grads"], f64["grads"])
+    print(f"\nC2 UNet fp32 4x512^2: logits max|d| {e:.2e}; argmax flips {near} near-tie / {hard} other; confusion |d| "
+          f"{cm_diff}; loss {loss:.7f} vs {c32['loss']:.7f}; grads vs fp64: ours worst {w_h:.2e} ({k_h}) rel-L2 "
+          f"{r_h:.2e}, CPU fp32 oracle worst {w_c:.2e} ({k_c}) rel-L2 {r_c:.2e}")
+    assert e <= 1e-4, e
+    assert hard == 0, hard
+    assert cm_diff <= 2 * near, (cm_diff, near)
+    assert abs(loss - c32["loss"]) <= 1e-5 * abs(c32["loss"])
+    assert w_h <= 1.5 * w_c + 1e-4, (w_h, k_h, w_c)
+    assert r_h <= 1.5 * r_c + 1e-4, (r_h, r_c)
+    bufs = dict(m.named_buffers())
+    for k, b in c32["bufs"].items():
+        assert float((bufs[k].float().cpu() - b.float()).abs().max()) <= 1e-4 * (1 + float(b.float().abs().max())), k
+    m.eval()
+    with torch.no_grad():
+        ev = m(ref["x"].cuda())
+    ee = float((ev.double().cpu() - c32["eval"]).abs().max())
+    assert ee <= 1e-4 * (1 + float(c32["eval"].abs().max())), ee
+
+
+def test_c2_unet_bf16_vs_oracle(c2_ref):
+    """bf16 at C2 with the benchmark's conv3 tiles asserted; gated like C3 against PyTorch's own bf16."""
+    ref, f64, ac = c2_ref, c2_ref["f64"], c2_ref["ac16"]
+    log = []
+    m, out, loss, grads = hip_run(ref["init"], ref["x"], ref["t"], "bf16", kind="unet", log=log)
+    names = _conv_kinds(log)
+    assert "conv3_kernel<bf16,3,1,4,1,8,1>" in names and "conv3_kernel<bf16,3,1,4,2,8,1>" in names, sorted(names)
+    assert "conv3_kernel<bf16,3,2,4,2,8,1>" in names and "conv3_kernel<bf16,3,2,4,1,8,1>" in names, sorted(names)
+    assert not any(n.startswith(("conv2_kernel", "conv_generic")) for n in names), sorted(names)
+    print()
+    e, agree, lrel, r = report16("C2 bf16 HIP     ", out, loss, grads, f64)
+    e_a, agree_a, _, r_a = report16("C2 bf16 autocast", ac["out"], ac["loss"], ac["grads"], f64)
+    assert e <= 1.1 * e_a + 5e-3 and e <= 0.2, (e, e_a)
+    assert agree >= agree_a - 5e-3 and agree >= 0.95, (agree, agree_a)
+    assert lrel <= 1e-2, lrel
+    assert r <= 1.1 * r_a + 2e-2 and r <= 0.7, (r, r_a)
+
+
+# ------------------------------------------------------------------------------------------------
+# the discriminating 16-bit gate: eval-mode BN, full size, forward + backward vs fp64
+# ------------------------------------------------------------------------------------------------
+_EVAL_REFS = {}
+
+
+def _eval_ref(kind):
+    if kind not in _EVAL_REFS:
+        init = seeded_init(kind, 1)
+        g = torch.Generator().manual_seed(2026 if kind == "unet" else 2024)
+        x = torch.rand(N, 1, S, S, generator=g) * 2 - 1
+        t = discs(N, S, S, g)
+        init = batch_running_stats(init, x, kind)
+        _EVAL_REFS[kind] = {
+            "init": init, "x": x, "t": t,
+            "f64": oracle_run(init, x, t, "cuda", torch.float64, kind=kind, training=False, want_eval=False),
+            "ac": {dt: oracle_run(init, x, t, "cuda", torch.float32, kind=kind, training=False, autocast=dt,
+                                  want_eval=False) for dt in (torch.bfloat16, torch.float16)},
+        }
+    return _EVAL_REFS[kind]
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("kind", ["unet", "attention"])
+def test_eval_mode_16bit_fwd_bwd_vs_fp64(kind, prec):
+    """C2 / C3 network at full size in eval mode (running statistics = one batch's statistics), forward +
+    DiceBCE + backward through the 16-bit kernels (conv3 y and dgrad tiles incl. the fused BN-backward sums,
+    wgrad2, the gate kernels, the pooled BN backward) against the fp64 oracle: logits and all-parameter
+    gradient rel-L2 <= 2e-2."""
+    _threads()
+    ref = _eval_ref(kind)
+    f64 = ref["f64"]
+    log = []
+    m, out, loss, grads = hip_run(ref["init"], ref["x"], ref["t"], prec, kind=kind, training=False, log=log)
+    names = _conv_kinds(log)
+    assert f"conv3_kernel<{prec},3,1,4,1,8,1>" in names and f"conv3_kernel<{prec},3,2,4,2,8,1>" in names, sorted(names)
+    ac = ref["ac"][torch.bfloat16 if prec == "bf16" else torch.float16]
+    print()
+    e, agree, lrel, r = report16(f"{kind} eval {prec} HIP     ", out, loss, grads, f64)
+    e_a, _, _, r_a = report16(f"{kind} eval {prec} autocast", ac["out"], ac["loss"], ac["grads"], f64)
+    assert e <= 2e-2, (e, e_a)
+    assert r <= 2e-2, (r, r_a)
+    assert lrel <= 2e-3, lrel
+    # per-layer: no single parameter's gradient far off (a mis-wired stage would be)
+    per = {k: rel_l2(grads[k], g) for k, g in f64["grads"].items() if float(g.norm()) > 0}
+    worst = max(per.items(), key=lambda kv: kv[1])
+    print(f"{kind} eval {prec}: worst per-tensor gradient rel-L2 {worst[1]:.3e} ({worst[0]})")
+    assert worst[1] <= 0.1, worst
+
+
+# ------------------------------------------------------------------------------------------------
+# fused BN-backward sums (dgrad y epilogue) vs the separate reduction
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("training", [True, False], ids=["train", "eval"])
+def test_bnb_epilogue_fused_vs_unfused(prec, training):
+    """AttentionUNet base 64, 2 x 256^2: every DoubleConv's middle BatchNorm backward sums either come from
+    its producing dgrad's epilogue (default) or from unet_bn_bwd_reduce (UNET_NO_BNB_FUSE=1)."""
+    from unet._hip import lib as L
+    torch.manual_seed(7)
+    init = seeded_init("attention", 1)
+    g = torch.Generator().manual_seed(8)
+    x = torch.rand(2, 1, 256, 256, generator=g) * 2 - 1
+    t = discs(2, 256, 256, g)
+    if not training:
+        init = batch_running_stats(init, x, "attention")
+    counts = []
+    runs = []
+    orig = L.call
+    for env in ({}, {"UNET_NO_BNB_FUSE": "1"}):
+        n = [0]
+
+        def rec(name, *args, n=n):
+            if name == "unet_bn_bwd_reduce":
+                n[0] += 1
+            return orig(name, *args)
+
+        L.call = rec
+        try:
+            runs.append(hip_run(init, x, t, prec, training=training, env=env))
+        finally:
+            L.call = orig
+        counts.append(n[0])
+    (m0, o0, l0, g0), (m1, o1, l1, g1) = runs
+    print(f"\nseparate BN-backward reductions: fused {counts[0]}, unfused {counts[1]}")
+    assert counts[1] - counts[0] >= 2, counts          # inc / up4 (64-channel middle maps at 256^2) fuse
+    assert torch.equal(o0, o1) and l0 == l1
+    bn_keys = [k for k in g0 if ".double_conv.1." in k]
+    worst_bn = max(float((g0[k] - g1[k]).abs().max()) / (float(g1[k].abs().max()) + 1e-30) for k in bn_keys)
+    w, k, r = grad_errs(g0, g1)
+    print(f"{prec} {'train' if training else 'eval'}: middle-BN grads worst max-norm diff {worst_bn:.2e}; all params "
+          f"rel-L2 {r:.2e}, worst {w:.2e} ({k})")
+    assert worst_bn <= 2e-3, worst_bn
+    assert r <= 1e-2, (r, k)
+
+
+# ------------------------------------------------------------------------------------------------
+# C5: AttentionUNet 3 x 1024^2, fp16
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def c5_ref():
+    init = seeded_init("attention", 3)
+    g = torch.Generator().manual_seed(2027)
+    x = torch.rand(2, 3, 1024, 1024, generator=g) * 2 - 1
+    t = discs(2, 1024, 1024, g)
+    return {"init": init, "x": x, "t": t,
+            "f64": oracle_run(init, x, t, "cuda", torch.float64, want_eval=False),
+            "ac16": oracle_run(init, x, t, "cuda", torch.float32, autocast=torch.float16, want_eval=False)}
+
+
+def test_c5_fp16_1024_vs_oracle(c5_ref):
+    """fp16 fwd + bwd at C5's image size (3 x 1024^2, base 64) with the 1024^2 conv3 tiles asserted,
+    against fp64 beside autocast-fp16; then a GradScaler step (init scale 2^16, backing off on overflow
+    as torch.amp does) whose unscaled gradients meet the same gate."""
+    ref, f64, ac = c5_ref, c5_ref["f64"], c5_ref["ac16"]
+    log = []
+    m, out, loss, grads = hip_run(ref["init"], ref["x"], ref["t"], "fp16", in_ch=3, log=log)
+    names = _conv_kinds(log)
+    for k in ("conv3_kernel<fp16,3,1,4,1,8,1>", "conv3_kernel<fp16,3,1,4,2,8,1>", "conv3_kernel<fp16,3,2,4,2,8,1>",
+              "conv3_kernel<fp16,3,2,4,1,8,1>", "smallcin_fwd_kernel<fp16>"):
+        assert k in names, (k, sorted(names))
+    print()
+    e, agree, lrel, r = report16("C5 fp16 HIP     ", out, loss, grads, f64)
+    e_a, agree_a, _, r_a = report16("C5 fp16 autocast", ac["out"], ac["loss"], ac["grads"], f64)
+    assert e <= 1.1 * e_a + 5e-3 and e <= 0.2, (e, e_a)
+    assert agree >= agree_a - 5e-3 and agree >= 0.95, (agree, agree_a)
+    assert lrel <= 1e-2, lrel
+    assert r <= 1.1 * r_a + 2e-2 and r <= 0.7, (r, r_a)
+    # GradScaler (scripts/train.py with fp16 autocast would use torch.amp.GradScaler)
+    from unet.utils.loss import DiceBCELoss
+    scaler = torch.amp.GradScaler("cuda")
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4)
+    before = {k: p.detach().clone() for k, p in m.named_parameters()}
+    taken = False
+    for _ in range(4):
+        opt.zero_grad(set_to_none=True)
+        scale = scaler.get_scale()
+        o = m(ref["x"].cuda())
+        scaler.scale(DiceBCELoss()(o, ref["t"].cuda())).backward()
+        scaler.unscale_(opt)
+        sg = {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()}
+        finite = all(torch.isfinite(v).all() for v in sg.values())
+        scaler.step(opt)
+        scaler.update()
+        if finite:
+            taken = True
+            break
+        assert scaler.get_scale() < scale      # overflow detected: step skipped, scale backed off
+    assert taken
+    _, _, r_s = grad_errs(sg, f64["grads"])
+    print(f"C5 GradScaler step at scale {scale:.0f}: unscaled grads rel-L2 vs fp64 {r_s:.3e}")
+    assert r_s <= 1.1 * r_a + 2e-2, (r_s, r_a)
+    changed = sum(int(not torch.equal(p.detach(), before[k])) for k, p in m.named_parameters())
+    assert changed == len(before)

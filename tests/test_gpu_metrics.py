@@ -106,3 +106,22 @@ def test_iou_dice_count_every_pixel(C, K):
     ri, rd = O.class_iou_dice(p, t, K)
     assert torch.equal(compute_iou(p.cuda(), t.cuda(), K).cpu(), ri)
     assert torch.equal(compute_dice(p, t, K).cpu(), rd)
+
+
+@pytest.mark.parametrize("C,K", [(3, 2), (2, 3), (5, 2)])
+def test_update_logits_channels_differ_from_num_classes(C, K):
+    """SegmentationMetrics.update with logits whose channel count C != num_classes: the reference takes the
+    argmax over all C channels and skips pixels whose class (target or prediction) is outside [0, K)
+    (metrics.py:68-84); the device kernel does the same (unet_confusion_matrix with C and K)."""
+    from unet.utils.metrics import SegmentationMetrics
+    O = _o()
+    gen = torch.Generator().manual_seed(40 + C * 7 + K)
+    z = torch.randn(2, C, 37, 53, generator=gen)
+    t = torch.randint(0, max(C, K) + 1, (2, 37, 53), generator=gen)
+    m = SegmentationMetrics(num_classes=K)
+    m.update(z.cuda(), t.cuda())
+    m.update(z, t)                          # host tensors too
+    p = z.argmax(1)
+    keep = (t >= 0) & (t < K) & (p >= 0) & (p < K)
+    ref = O.confusion_matrix(p[keep], t[keep], K) * 2
+    assert np.array_equal(m.get_confusion_matrix(), ref.numpy())

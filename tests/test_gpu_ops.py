@@ -499,7 +499,8 @@ Y_BENCH = [
 @pytest.mark.parametrize("shape", Y_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
 @pytest.mark.parametrize("stats", [True, False])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv3_bench_tiles_y(prec, shape, stats):
+def test_conv3_bench_tiles_y(prec, shape, stats, monkeypatch):
+    monkeypatch.setenv("UNET_CONV4", "0")   # the conv3 tiles (conv4: test_gpu_conv4.py)
     L = _lib()
     N, H, W, cin, cout, want = shape
     dt = DT[prec]
@@ -543,7 +544,8 @@ DGRAD_BENCH = [
 
 @pytest.mark.parametrize("shape", DGRAD_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv3_bench_tiles_dgrad_f32(prec, shape):
+def test_conv3_bench_tiles_dgrad_f32(prec, shape, monkeypatch):
+    monkeypatch.setenv("UNET_CONV4", "0")   # the conv3 tiles (conv4: test_gpu_conv4.py)
     L = _lib()
     N, H, W, cin, cout, want = shape
     dt = DT[prec]
@@ -567,8 +569,9 @@ def test_conv3_bench_tiles_dgrad_f32(prec, shape):
 @pytest.mark.parametrize("shape", [(4, 512, 512, 64, 64), (4, 256, 256, 128, 128), (3, 200, 328, 64, 64)],
                          ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv3_bench_tiles_dgrad_y(prec, shape):
+def test_conv3_bench_tiles_dgrad_y(prec, shape, monkeypatch):
     """bf16 gradient of a DoubleConv's middle activation (the y epilogue without BN sums)."""
+    monkeypatch.setenv("UNET_CONV4", "0")   # the conv3 tiles (conv4: test_gpu_conv4.py)
     L = _lib()
     N, H, W, cin, cout = shape
     dt = DT[prec]
@@ -704,25 +707,36 @@ def test_wgrad_source_kinds(prec, shape, kind):
     assert rel <= 2e-3, rel    # the gate / activation rounding to bf16 can differ by one ulp from torch's
 
 
+@pytest.mark.parametrize("path", ["conv4", "conv3"])
+@pytest.mark.parametrize("regime", ["centered", "offset"])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("shape", [(4, 256, 256, 64, 64), (4, 128, 128, 128, 128), (2, 64, 64, 256, 256),
                                    (1, 24, 40, 64, 64), (2, 20, 36, 36, 20), (3, 33, 20, 96, 128)],
                          ids=lambda s: "x".join(map(str, s)))
-def test_dgrad_y_bn_backward_sums(prec, shape):
+def test_dgrad_y_bn_backward_sums(prec, shape, regime, path, monkeypatch):
     """The dgrad y epilogue's fused BatchNorm-backward reduction (unet_conv_desc.bnb_*): per channel
     Σg and Σg·(y-mean)·invstd of the STORED gradient g, masked by the activation's ReLU, against torch
-    on the same stored values (conv3 / conv2 epilogues and the fallback reduction of the other paths)."""
+    on the same stored values (conv3 / conv2 epilogues and the fallback reduction of the other paths).
+    regime "offset": y = 50 + N(0, 1) with mean ≈ 50 (|mean| >> std), where the epilogue's
+    invstd·(Σg·y − mean·Σg) form cancels; its error must stay at fp32 summation-noise level relative to
+    Σ|g·(y − mean)·invstd|."""
+    monkeypatch.setenv("UNET_CONV4", "1" if path == "conv4" else "0")
     L, R = _lib(), _rt()
     N, H, W, cmid, cout = shape     # the conv cmid -> cout; its dgrad writes the cmid-channel gradient
     dt = DT[prec]
     torch.manual_seed(21)
     dy = _rand(N, H, W, cout, dt=dt)
     w = (torch.randn(cout, cmid, 3, 3, device="cuda") * (2.0 / (9 * cmid)) ** 0.5).to(dt).float()
-    y1 = _rand(N, H, W, cmid, dt=dt)
     sc = torch.rand(cmid, device="cuda") + 0.5
-    sf = torch.randn(cmid, device="cuda") * 0.3
+    if regime == "offset":
+        y1 = (50.0 + torch.randn(N, H, W, cmid, device="cuda")).to(dt)
+        mean = 50.0 + torch.randn(cmid, device="cuda") * 0.1
+        sf = -sc * 50.0 + torch.randn(cmid, device="cuda") * 0.3     # the ReLU keeps about half
+    else:
+        y1 = _rand(N, H, W, cmid, dt=dt)
+        mean = torch.randn(cmid, device="cuda") * 0.1
+        sf = torch.randn(cmid, device="cuda") * 0.3
     ab = torch.stack([sc, sf])
-    mean = torch.randn(cmid, device="cuda") * 0.1
     invstd = torch.rand(cmid, device="cuda") + 0.5
     src = L.Src()
     src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
@@ -756,6 +770,11 @@ def test_dgrad_y_bn_backward_sums(prec, shape):
     for k, (a, b) in enumerate(((got[0], s1), (got[1], s2))):
         scale = gm.abs().sum(0) * (1 if k == 0 else float((yv - mean.double()).abs().max() * invstd.max()))
         assert ((a - b).abs() <= 1e-5 * scale + 1e-4).all(), (k, float((a - b).abs().max()), _variant(d))
+    # against the natural scale of the second sum (the sum of its absolute terms)
+    nat = (gm * (yv - mean.double()) * invstd.double()).abs().sum(0)
+    rel = float(((got[1] - s2).abs() / (nat + 1e-30)).max())
+    print(f" {regime}: Σg·x̂ max error / Σ|g·x̂| = {rel:.2e} ({_variant(d)})")
+    assert rel <= 2e-5, (rel, _variant(d))
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])

@@ -92,14 +92,18 @@ __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long lon
   }
 }
 
+// eval mode: the running-statistics affine; mean / invstd (optional) are what the backward of an eval-mode
+// forward normalises with (x̂ = (y - running_mean) * invstd)
 __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
-                               float* scale, float* shift) {
+                               float* scale, float* shift, float* mean, float* invstd) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const float is = 1.0f / sqrtf(rv[c] + eps);
   const float sc = gamma[c] * is;
   scale[c] = sc;
   shift[c] = beta[c] - rm[c] * sc;
+  if (mean) mean[c] = rm[c];
+  if (invstd) invstd[c] = is;
 }
 
 // 2-D layout: CL channel lanes x (256/CL) pixel rows; grid (ceil(C/CL), rows)
@@ -298,7 +302,8 @@ static inline int reduce_rows_vec(long long P, int C) {
   return (int)r;
 }
 
-// one block per channel: sums over rows in fp64
+// one block per channel: sums over rows in fp64.  count == 0: eval mode (running statistics are constants
+// of the forward), so dy = γ·invstd·g: coef = (γ·invstd, 0, 0)
 __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
                                        const float* gamma, const float* mean, const float* invstd, float* dgamma,
                                        float* dbeta, int accum, float* coef) {
@@ -325,11 +330,16 @@ __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, 
     if (dgamma) dgamma[c] = accum ? dgamma[c] + (float)b : (float)b;
     if (coef) {
       const double k = (double)gamma[c] * invstd[c];
-      const double M = (double)count;
-      const double B = -k * (double)invstd[c] * b / M;
       coef[c] = (float)k;
-      coef[C + c] = (float)B;
-      coef[2 * C + c] = (float)(-k * a / M - B * (double)mean[c]);
+      if (count > 0) {
+        const double M = (double)count;
+        const double B = -k * (double)invstd[c] * b / M;
+        coef[C + c] = (float)B;
+        coef[2 * C + c] = (float)(-k * a / M - B * (double)mean[c]);
+      } else {
+        coef[C + c] = 0.f;
+        coef[2 * C + c] = 0.f;
+      }
     }
   }
 }
@@ -381,9 +391,13 @@ int unet_bn_finalize(const float* stats, int rows, int C, long long count, const
 }
 
 int unet_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
-                        float* scale, float* shift, void* stream) {
+                        float* scale, float* shift, float* mean, float* invstd, void* stream) {
+  if (C <= 0 || !gamma || !beta || !rm || !rv || !scale || !shift) {
+    set_error("unet_bn_eval_affine: bad args");
+    return UNET_ERR_ARG;
+  }
   hipLaunchKernelGGL(bn_eval_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, C, gamma, beta, rm, rv,
-                     eps, scale, shift);
+                     eps, scale, shift, mean, invstd);
   return check_launch("bn_eval_affine");
 }
 
@@ -436,6 +450,10 @@ int unet_bn_bwd_reduce(int dtype, int da_dtype, long long P, int C, const void* 
 int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int C, long long count, const float* gamma,
                          const float* mean, const float* invstd, float* dgamma, float* dbeta, int accum, float* coef,
                          void* stream) {
+  if (!sum_g || !sum_gx || rows <= 0 || C <= 0 || count < 0 || (coef && (!gamma || !invstd || (count > 0 && !mean)))) {
+    set_error("unet_bn_bwd_finalize: bad args");
+    return UNET_ERR_ARG;
+  }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(fin_threads(rows)), 0, (hipStream_t)stream, sum_g, sum_gx, rows, C, count,
                      gamma, mean, invstd, dgamma, dbeta, accum, coef);
   return check_launch("bn_bwd_finalize");

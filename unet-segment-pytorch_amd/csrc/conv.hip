@@ -15,7 +15,7 @@
 //  * Epilogue: y (NHWC) + per-tile BN partial sums, or fp32 gradients (channel split for the concat,
 //    or routed through the 2x2 max-pool argmax).
 #include <stdio.h>
-#include "halo_items.h"
+#include "conv_src16.h"
 
 namespace unet {
 
@@ -483,6 +483,10 @@ static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t s
 #include "conv3_body.inc"
 
 template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
+bool conv4_eligible(const unet_conv_desc* d);   // conv4.hip: the 32x32x16-MFMA 3x3 path
+int conv4_run(const unet_conv_desc* d, hipStream_t st);
+int conv4_stats_rows(const unet_conv_desc* d);
+int conv4_variant(const unet_conv_desc* d, char* buf, int len);
 bool smallcin_conv_ok(const unet_conv_desc* d);  // smallcin.hip
 bool pw_conv_ok(const unet_conv_desc* d);        // pw.hip
 int pw_conv_rows(const unet_conv_desc* d);
@@ -507,6 +511,9 @@ static bool fast_eligible(const unet_conv_desc* d) {
 template <typename T>
 static int dispatch_conv(const unet_conv_desc* d, hipStream_t st) {
   if (!fast_eligible(d)) return dispatch_generic<T>(d, st);
+  if constexpr (sizeof(T) == 2) {
+    if (conv4_eligible(d)) return conv4_run(d, st);
+  }
   const ConvCfg c = pick_cfg(d);
   if constexpr (sizeof(T) == 2) {
     if (conv3_eligible(d)) return dispatch_conv3<T>(d, c, st);
@@ -593,6 +600,7 @@ int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8)
 // does unet_conv reduce d's bnb_* sums in the conv epilogue (rows = the conv's M tiles)?
 static bool bnb_in_epilogue(const unet_conv_desc* d) {
   if (smallcin_conv_ok(d) || pw_conv_ok(d) || !fast_eligible(d) || d->dtype == UNET_F32) return false;
+  if (conv4_eligible(d)) return true;
   return conv3_bnb_tile(d, pick_cfg(d));
 }
 
@@ -601,6 +609,7 @@ int unet_conv_stats_rows(const unet_conv_desc* d) {
   if (smallcin_conv_ok(d)) return smallcin_rows((long long)d->N * d->H * d->W);
   if (pw_conv_ok(d)) return pw_conv_rows(d);
   if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
+  if (conv4_eligible(d)) return conv4_stats_rows(d);
   const ConvCfg c = pick_cfg(d);
   return d->N * cdiv(d->W, CTW) * cdiv(d->H, 4 * c.wm);
 }
@@ -616,6 +625,7 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
              d->Cout <= 32 ? 32 : 64);
     return 0;
   }
+  if (conv4_eligible(d)) return conv4_variant(d, buf, len);
   const ConvCfg c = pick_cfg(d);
   if (conv3_eligible(d)) {
     // the (wm, wn, ntn) block tile of pick_cfg; 16-row tiles run as MI=8 waves (dispatch_conv3)

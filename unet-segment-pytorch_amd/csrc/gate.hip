@@ -92,8 +92,7 @@ __global__ void gate_bwd1_kernel(long long P, int Cx, const float* dxs, const T*
       const float dv = d[c];
       ds += dv * xv;
       if (dx) {
-        const float g = dv * sg;
-        o[c] = dx_accum ? o[c] + g : g;
+        o[c] = dx_accum ? __builtin_fmaf(dv, sg, o[c]) : dv * sg;
       }
     }
     const float dqv = ds * sg * (1.f - sg);
@@ -209,9 +208,9 @@ __global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* dx
         if (relu) xv = fmaxf(xv, 0.f);
         ds += d[u][j] * xv;
       }
-      if (dx_accum) {
+      if (dx_accum) {  // one rounding (explicit fmaf), the operation the gated W_x dgrad epilogue uses
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[u][j] += d[u][j] * sg;
+        for (int j = 0; j < 8; ++j) g[u][j] = __builtin_fmaf(d[u][j], sg, g[u][j]);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[u][j] = d[u][j] * sg;

@@ -75,14 +75,15 @@ static int launch_confusion(int ext, long long N, int C, int K, long long HW, co
   return check_launch("confusion_matrix");
 }
 
-extern "C" int unet_confusion_matrix(long long N, int K, long long HW, const float* logits, const int64_t* labels,
-                                     const int64_t* targets, long long ignore_index, int has_ignore,
-                                     int64_t* confusion, void* stream) {
-  if (N <= 0 || HW <= 0 || K < 1 || K > CM_MAXK || (!logits && !labels) || !targets || !confusion) {
-    set_error("unet_confusion_matrix: bad arguments (1 <= num_classes <= 8)");
+extern "C" int unet_confusion_matrix(long long N, int C, int K, long long HW, const float* logits,
+                                     const int64_t* labels, const int64_t* targets, long long ignore_index,
+                                     int has_ignore, int64_t* confusion, void* stream) {
+  if (N <= 0 || HW <= 0 || K < 1 || K > CM_MAXK || (logits && C < 1) || (!logits && !labels) || !targets ||
+      !confusion) {
+    set_error("unet_confusion_matrix: bad arguments (1 <= num_classes <= 8, C >= 1)");
     return UNET_ERR_ARG;
   }
-  return launch_confusion(0, N, K, K, HW, logits, labels, targets, ignore_index, has_ignore, confusion, stream);
+  return launch_confusion(0, N, C, K, HW, logits, labels, targets, ignore_index, has_ignore, confusion, stream);
 }
 
 extern "C" int unet_confusion_matrix_ext(long long N, int C, int K, long long HW, const float* logits,

@@ -20,6 +20,12 @@ from .runtime import (Act, act_from_nchw, act_to_nchw, f32, get_precision, grad_
 from .stages import (DoubleConvStage, DownStage, GateStage, Grads, NetworkPlan, OutConvStage, UpStage)
 
 
+# the plan's activation-gradient buffers and packed dgrad weights are consumed by the first backward
+_SECOND_BACKWARD = ("unet HIP path: this graph was already backpropagated; the HIP network does not support a "
+                    "second backward through the same forward (retain_graph=True / autograd.grad then backward). "
+                    "Run the forward again.")
+
+
 class _PlanFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, plan, params: Sequence[torch.nn.Parameter], n_in: int, *tensors):
@@ -33,6 +39,8 @@ class _PlanFn(torch.autograd.Function):
     @staticmethod
     @once_differentiable
     def backward(ctx, *gouts):
+        if ctx.plan is None:
+            raise RuntimeError(_SECOND_BACKWARD)
         grads = Grads()
         dins = ctx.plan.backward(list(gouts), grads)
         pgrads = [grads.get(p) for p in ctx.params]
@@ -71,6 +79,8 @@ class _StageFn(torch.autograd.Function):
     @once_differentiable
     def backward(ctx, *gouts):
         st = ctx.st
+        if st is None:
+            raise RuntimeError(_SECOND_BACKWARD)
         grads = Grads()
         dins = st.bwd(list(gouts), grads)
         ctx.st = None

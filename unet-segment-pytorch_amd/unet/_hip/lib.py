@@ -64,7 +64,7 @@ _SIGS = {
     "unet_conv_wgrad": (c_int, [ctypes.POINTER(WgradDesc), c_vp]),
     "unet_bn_finalize": (c_int, [c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_vp, c_vp,
                                  c_vp, c_vp, c_vp]),
-    "unet_bn_eval_affine": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_vp]),
+    "unet_bn_eval_affine": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "unet_bn_bwd_reduce_rows": (c_int, [c_ll, c_int]),
     "unet_bn_bwd_reduce": (c_int, [c_int, c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "unet_bn_bwd_finalize": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
@@ -104,7 +104,7 @@ _SIGS = {
     "unet_fill_f32": (c_int, [c_vp, c_ll, c_float, c_vp]),
     "unet_materialize": (c_int, [c_int, ctypes.POINTER(Src), c_ll, c_int, c_int, c_vp, c_vp]),
     "unet_materialize_pool": (c_int, [c_int, ctypes.POINTER(Src), c_ll, c_int, c_int, c_vp, c_vp, c_vp]),
-    "unet_confusion_matrix": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp]),
+    "unet_confusion_matrix": (c_int, [c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp]),
     "unet_confusion_matrix_ext": (c_int, [c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "unet_loss_rows": (c_int, [c_ll]),
     "unet_loss_reduce": (c_int, [c_ll, c_int, c_ll, c_vp, c_vp, c_vp, c_vp]),

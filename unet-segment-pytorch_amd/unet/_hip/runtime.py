@@ -59,7 +59,8 @@ class KernelProbe:
         self.records = []   # (start_event, end_event, algorithmic_flops)
         self.log = None     # when a list: every probed launch appends (kernel name, output mode)
 
-    def enable(self, target: str):
+    def enable(self, target):
+        """target: a kernel-name prefix, or a tuple of prefixes (a kernel family)"""
         self.target = target
         self.records = []
 
@@ -184,7 +185,7 @@ class Act:
     for a single-consumer activation in bf16 mode (`grad_single`)."""
 
     __slots__ = ("data", "N", "H", "W", "C", "ab", "relu", "mean", "invstd", "grad", "_grad_init", "keep",
-                 "bn_owned", "pool_grad")
+                 "bn_owned", "pool_grad", "batch_stats")
 
     def __init__(self, data: torch.Tensor, ab: Optional[torch.Tensor], relu: bool,
                  mean: Optional[torch.Tensor] = None, invstd: Optional[torch.Tensor] = None):
@@ -201,6 +202,7 @@ class Act:
         # fold a Down block's pooled gradient (pool_grad = (g2, code, ph, pw)) in on the fly
         self.bn_owned = False
         self.pool_grad = None
+        self.batch_stats = True   # False: an eval-mode BN (running statistics) produced it
 
     @property
     def scale(self):

@@ -1,9 +1,12 @@
 """Stage executor: the reference's modules re-expressed as HIP launches on virtual activations.
 
 Each stage mirrors one reference module (file:line in the docstrings) and owns the kernel launches
-for its forward and backward.  Inter-module transforms (BN-apply + ReLU of the previous
-DoubleConv, MaxPool2d, bilinear up, pad, concat, attention multiply) are not launched at all: they
-are folded into the consuming conv's tile loader through `unet_src` descriptors.
+for its forward and backward.  The BN-apply + ReLU of the previous DoubleConv, the zero pad, the
+channel concat and the attention multiply are not launched at all: they are folded into the
+consuming conv's tile loader through `unet_src` descriptors.  Two derived maps are written once per
+step instead (measured faster than a 4-corner gather inside the MFMA kernels): the 2x2 max-pooled
+input of each Down block (`unet_materialize_pool`, with 1-byte argmax codes for the backward) and
+the bilinear x2 upsample of each Up block's decoder input (`unet_materialize`).
 """
 
 from __future__ import annotations
@@ -86,10 +89,9 @@ class ConvBN:
             d.stats = stats.data_ptr()
         probe.launch(lambda: conv_kernel_name(d), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
                      lambda: L.call("unet_conv", d, stream()), d.out_mode)
-        mean = invstd = None
+        mean = f32(self.cout, device=dev)
+        invstd = f32(self.cout, device=dev)
         if use_batch:
-            mean = f32(self.cout, device=dev)
-            invstd = f32(self.cout, device=dev)
             upd = training and bn.track_running_stats
             mom = -1.0 if bn.momentum is None else float(bn.momentum)
             L.call("unet_bn_finalize", vp(stats), mt, self.cout, N * H * W, vp(bn.weight), vp(bn.bias),
@@ -97,9 +99,12 @@ class ConvBN:
                    vp(bn.num_batches_tracked) if upd else None, mom, float(bn.eps), vp(mean), vp(invstd),
                    vp(ab[0]), vp(ab[1]), stream())
         else:
+            # eval mode (running statistics): mean / invstd are the running ones, which the backward of an
+            # eval-mode forward treats as constants (unet_bn_bwd_finalize with count 0)
             L.call("unet_bn_eval_affine", self.cout, vp(bn.weight), vp(bn.bias), vp(bn.running_mean),
-                   vp(bn.running_var), float(bn.eps), vp(ab[0]), vp(ab[1]), stream())
+                   vp(bn.running_var), float(bn.eps), vp(ab[0]), vp(ab[1]), vp(mean), vp(invstd), stream())
         a = Act(y, ab, self.relu, mean, invstd)
+        a.batch_stats = use_batch
         a.keep = keep  # keeps the source tensors alive until backward
         a.bn_owned = True
         return a
@@ -131,7 +136,7 @@ class ConvBN:
             L.call("unet_bn_bwd_reduce", prec.code, gcode, P, C, vp(a.grad), vp(a.data), vp(a.ab[0]),
                    vp(a.ab[1]), int(a.relu), vp(a.mean), vp(a.invstd), vp(part), stream())
         dgamma, dbeta, coef = f32(C, device=dev), f32(C, device=dev), f32(3, C, device=dev)
-        L.call("unet_bn_bwd_finalize", vp(part[0]), vp(part[1]), rows, C, P, vp(self.bn.weight), vp(a.mean),
+        L.call("unet_bn_bwd_finalize", vp(part[0]), vp(part[1]), rows, C, P if a.batch_stats else 0, vp(self.bn.weight), vp(a.mean),
                vp(a.invstd), vp(dgamma), vp(dbeta), 0, vp(coef), stream())
         grads.put(self.bn.weight, dgamma)
         grads.put(self.bn.bias, dbeta)
@@ -236,7 +241,8 @@ class DoubleConvStage:
             # BN-backward reads
             # BN1's backward sums are reduced by that dgrad's epilogue (no separate pass over g1 and y1)
             g1 = self.a1.grad_single(prec.torch_dtype)
-            route = {"mode": "y", "out": g1, "bnb": self.a1 if self.a1.mean is not None else None}
+            # (env UNET_NO_BNB_FUSE: A/B switch back to the separate unet_bn_bwd_reduce pass)
+            route = {"mode": "y", "out": g1, "bnb": None if os.environ.get("UNET_NO_BNB_FUSE") else self.a1}
             self.c2.conv_backward(prec, dy2, [self.a1.src()], grads, route)
             fused = route.get("bnb_part")
         else:
@@ -285,8 +291,9 @@ class GateStage:
         bn = self.psi_bn
         self.psi_ab = f32(2, 1, device=dev)
         use_batch = training or not bn.track_running_stats
+        self.psi_batch = use_batch
+        self.psi_mean, self.psi_invstd = f32(1, device=dev), f32(1, device=dev)
         if use_batch:
-            self.psi_mean, self.psi_invstd = f32(1, device=dev), f32(1, device=dev)
             upd = training and bn.track_running_stats
             mom = -1.0 if bn.momentum is None else float(bn.momentum)
             L.call("unet_bn_finalize", vp(part), rows, 1, P, vp(bn.weight), vp(bn.bias),
@@ -295,7 +302,8 @@ class GateStage:
                    vp(self.psi_invstd), vp(self.psi_ab[0]), vp(self.psi_ab[1]), stream())
         else:
             L.call("unet_bn_eval_affine", 1, vp(bn.weight), vp(bn.bias), vp(bn.running_mean), vp(bn.running_var),
-                   float(bn.eps), vp(self.psi_ab[0]), vp(self.psi_ab[1]), stream())
+                   float(bn.eps), vp(self.psi_ab[0]), vp(self.psi_ab[1]), vp(self.psi_mean), vp(self.psi_invstd),
+                   stream())
 
     def _forward_eval(self, prec, g_up_t: torch.Tensor, x: Act):
         """Eval mode, no autograd (predict.py): BN on running statistics, so psi's pre-activation is
@@ -308,7 +316,7 @@ class GateStage:
         gab, xab = f32(2, ci, device=dev), f32(2, ci, device=dev)
         for bn, ab in ((self.cg.bn, gab), (self.cx.bn, xab)):
             L.call("unet_bn_eval_affine", ci, vp(bn.weight), vp(bn.bias), vp(bn.running_mean), vp(bn.running_var),
-                   float(bn.eps), vp(ab[0]), vp(ab[1]), stream())
+                   float(bn.eps), vp(ab[0]), vp(ab[1]), None, None, stream())
         self.wpsi = self.psi_conv.weight.detach().reshape(-1).float().contiguous()
         self.p = f32(x.N, x.H, x.W, device=dev)
         L.call("unet_gate_psi_eval", prec.code, x.pixels, g_up_t.shape[-1], x.C, ci, vp(g_up_t), vp(x.data),
@@ -317,7 +325,7 @@ class GateStage:
         bn = self.psi_bn
         self.psi_ab = f32(2, 1, device=dev)
         L.call("unet_bn_eval_affine", 1, vp(bn.weight), vp(bn.bias), vp(bn.running_mean), vp(bn.running_var),
-               float(bn.eps), vp(self.psi_ab[0]), vp(self.psi_ab[1]), stream())
+               float(bn.eps), vp(self.psi_ab[0]), vp(self.psi_ab[1]), None, None, stream())
 
     def gated_src(self) -> L.Src:
         return self.x.src_gated(self.p, self.psi_ab)
@@ -339,7 +347,8 @@ class GateStage:
         L.call("unet_gate_bwd1", prec.code, P, Cx, vp(d_xs), vp(x.data), vp(x.ab[0]), vp(x.ab[1]), int(x.relu), vp(self.p),
                vp(self.psi_ab), vp(self.psi_mean), vp(self.psi_invstd), vp(dx), dx_acc, vp(dq), vp(part1), stream())
         dgp, dbp, pcoef = f32(1, device=dev), f32(1, device=dev), f32(3, device=dev)
-        L.call("unet_bn_bwd_finalize", vp(part1[0]), vp(part1[1]), rows1, 1, P, vp(self.psi_bn.weight),
+        L.call("unet_bn_bwd_finalize", vp(part1[0]), vp(part1[1]), rows1, 1, P if self.psi_batch else 0,
+               vp(self.psi_bn.weight),
                vp(self.psi_mean), vp(self.psi_invstd), vp(dgp), vp(dbp), 0, vp(pcoef), stream())
         grads.put(self.psi_bn.weight, dgp)
         grads.put(self.psi_bn.bias, dbp)
@@ -351,9 +360,11 @@ class GateStage:
                vp(self.wpsi), vp(dq), vp(self.p), vp(pcoef), vp(part2), stream())
         dgg, dbg, gcoef = f32(Ci, device=dev), f32(Ci, device=dev), f32(3, Ci, device=dev)
         dgx, dbx, xcoef = f32(Ci, device=dev), f32(Ci, device=dev), f32(3, Ci, device=dev)
-        L.call("unet_bn_bwd_finalize", vp(part2[0]), vp(part2[1]), rows2, Ci, P, vp(self.cg.bn.weight),
+        L.call("unet_bn_bwd_finalize", vp(part2[0]), vp(part2[1]), rows2, Ci, P if self.gw.batch_stats else 0,
+               vp(self.cg.bn.weight),
                vp(self.gw.mean), vp(self.gw.invstd), vp(dgg), vp(dbg), 0, vp(gcoef), stream())
-        L.call("unet_bn_bwd_finalize", vp(part2[0]), vp(part2[2]), rows2, Ci, P, vp(self.cx.bn.weight),
+        L.call("unet_bn_bwd_finalize", vp(part2[0]), vp(part2[2]), rows2, Ci, P if self.xw.batch_stats else 0,
+               vp(self.cx.bn.weight),
                vp(self.xw.mean), vp(self.xw.invstd), vp(dgx), vp(dbx), 0, vp(xcoef), stream())
         grads.put(self.cg.bn.weight, dgg)
         grads.put(self.cg.bn.bias, dbg)

@@ -1,8 +1,10 @@
 """UNet / AttentionUNet with the reference's API (unet/models/unet.py of seagochen/unet-segment-pytorch).
 
-The whole network runs as one HIP launch plan (`unet._hip.stages.NetworkPlan`) so that every
-BN-apply/ReLU/max-pool/upsample/pad/concat/attention-multiply between modules is fused into the
-next convolution's tile loader; module boundaries exist only in the parameter tree.
+The whole network runs as one HIP launch plan (`unet._hip.stages.NetworkPlan`): the BN-apply/ReLU/
+pad/concat/attention-multiply between modules is fused into the next convolution's tile loader, and
+the max-pooled / bilinear-upsampled maps are written once each (`unet_materialize_pool` /
+`unet_materialize`) and read plain.  Autograd sees one node per reference module (so DDP overlaps
+its all-reduces with the rest of the backward); the parameter tree is the reference's.
 """
 
 import torch

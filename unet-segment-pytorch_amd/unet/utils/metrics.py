@@ -46,18 +46,18 @@ def confusion_matrix(predictions: torch.Tensor, targets: torch.Tensor, num_class
     t = targets.to(torch.int64).contiguous()
     if predictions.dim() == 4:
         z = predictions.detach().float().contiguous()
+        # argmax over however many channels the logits have; a class >= K is then skipped like the
+        # reference's `0 <= p < num_classes` test (metrics.py:68-84)
         N, C, H, W = z.shape
-        if C != K:
-            raise ValueError(f"logits have {C} channels, metrics were set up for {K} classes")
         logits, labels = z.data_ptr(), None
     else:
         p = predictions.detach().to(torch.int64).contiguous()
         N = p.shape[0]
-        H, W = 1, p.numel() // max(N, 1)
+        C, H, W = 1, 1, p.numel() // max(N, 1)
         logits, labels = None, p.data_ptr()
     if t.numel() != N * H * W:
         raise ValueError(f"targets have {t.numel()} elements, predictions describe {N * H * W} pixels")
-    L.call("unet_confusion_matrix", N, K, H * W, logits, labels, t.data_ptr(),
+    L.call("unet_confusion_matrix", N, C, K, H * W, logits, labels, t.data_ptr(),
            int(ignore_index) if ignore_index is not None else 0, int(ignore_index is not None), out.data_ptr(),
            stream())
     return out
