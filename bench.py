@@ -93,6 +93,109 @@ def cpu_baseline(model_kind: str, size: int, batch: int, iters: int) -> dict:
                       f"1 warm-up + {iters} timed fwd+DiceBCE+bwd iterations ({dt:.1f} s)"}
 
 
+def _es(code: int) -> int:
+    return 4 if code == 0 else 2   # UNET_F32 = 0, UNET_BF16 = 1, UNET_F16 = 2
+
+
+def _hbm_bytes(name: str, a: tuple):
+    """(family, algorithmic HBM bytes) of one C-ABI call: every operand read once + every output written
+    once (include/unet_hip.h argument order), or None for calls that are not HBM-bound streaming kernels."""
+    if name == "unet_bn_bwd_apply":             # da, y -> dy
+        dt, gt, P, C = a[0], a[1], a[2], a[3]
+        return name, P * C * (_es(gt) + 2 * _es(dt))
+    if name == "unet_bn_bwd_reduce":            # da, y -> partial sums
+        dt, gt, P, C = a[0], a[1], a[2], a[3]
+        return name, P * C * (_es(gt) + _es(dt))
+    if name in ("unet_bn_bwd_reduce_pool", "unet_bn_bwd_apply_pool"):
+        dt, N, H, W, C, da, ph, pw = a[0], a[1], a[2], a[3], a[4], a[5], a[8], a[9]
+        b = N * H * W * C * _es(dt) + (N * H * W * C * 4 if da else 0) + N * ph * pw * C * 5
+        return name, b + (N * H * W * C * _es(dt) if name.endswith("apply_pool") else 0)
+    if name == "unet_gate_bwd1":                # dxs, y_x, p (+dx) -> dx?, dq
+        dt, P, C, dx, acc = a[0], a[1], a[2], a[12], a[13]
+        return name, P * C * (4 + _es(dt)) + 8 * P + (P * C * 4 * (2 if acc else 1) if dx else 0)
+    if name == "unet_gate_bwd2":
+        dt, P, C = a[0], a[1], a[2]
+        return name, 2 * P * C * _es(dt) + 8 * P
+    if name == "unet_gate_bwd3":
+        dt, P, C = a[0], a[1], a[2]
+        return name, 4 * P * C * _es(dt) + 8 * P
+    if name == "unet_gate_psi":
+        dt, P, C = a[0], a[1], a[2]
+        return name, 2 * P * C * _es(dt) + 4 * P
+    if name == "unet_upsample_bwd":             # d_up (padded map) -> dx (source map)
+        N, C, Hs, Ws, Hp, Wp, acc = a[0], a[1], a[2], a[3], a[8], a[9], a[14]
+        return name, N * Hp * Wp * C * 4 + N * Hs * Ws * C * 4 * (2 if acc else 1)
+    if name in ("unet_materialize", "unet_materialize_pool"):
+        dt, src, N, H, W = a[0], a[1], a[2], a[3], a[4]
+        b = N * src.H * src.W * src.C * _es(dt) + N * H * W * src.C * _es(dt)
+        return name, b + (N * H * W * src.C if name.endswith("pool") else 0)
+    if name == "unet_conv":
+        from unet._hip.runtime import conv_kernel_name
+        d = a[0]
+        v = conv_kernel_name(d)
+        fam = v.split("<")[0]
+        if fam not in ("smallcin_fwd_kernel", "pw_conv_kernel"):
+            return None
+        P = d.N * d.H * d.W
+        rd = sum(P * d.src[i].C * (4 if d.src[i].kind == 4 else _es(d.dtype)) for i in range(d.nsrc))
+        if d.out_mode == 0:
+            wr = P * d.Cout * _es(d.dtype)
+        else:   # fp32 gradient (accumulated: read too); gated: + d(x*s) and p read
+            wr = P * d.Cout * 4 * (2 if d.accum else 1) + (P * d.Cout * 4 + 4 * P if d.out_mode == 4 else 0)
+        return fam + ("" if d.out_mode == 0 else "(dgrad)"), rd + wr
+    return None
+
+
+class HbmProbe:
+    """Times the HBM-bound C-ABI calls of a step with HIP events on the launch stream (torch's current
+    stream, where every call is issued) and adds up their algorithmic bytes, per kernel family."""
+
+    def __init__(self):
+        from unet._hip import lib as L
+        self.L = L
+        self.rec = []
+        self.orig = None
+
+    def __enter__(self):
+        L, rec, orig = self.L, self.rec, self.L.call
+        self.orig = orig
+
+        def call(name, *args):
+            fb = _hbm_bytes(name, args)
+            if fb is None:
+                return orig(name, *args)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = orig(name, *args)
+            e.record()
+            rec.append((fb[0], fb[1], s, e))
+            return r
+
+        L.call = call
+        return self
+
+    def __exit__(self, *exc):
+        self.L.call = self.orig
+
+    def summary(self, traffic: dict):
+        torch.cuda.synchronize()
+        agg = {}
+        for fam, b, s, e in self.rec:
+            t = agg.setdefault(fam, [0, 0.0, 0.0])
+            t[0] += 1
+            t[1] += b
+            t[2] += s.elapsed_time(e) * 1e-3
+        out = {}
+        for fam, (n, b, sec) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+            gbs = b / sec / 1e9 if sec > 0 else None
+            m = traffic.get(fam)
+            out[fam] = {"launches": n, "algorithmic_bytes_per_launch": round(b / n),
+                        "avg_us": round(sec / n * 1e6, 2), "GBs": round(gbs, 1) if gbs else None,
+                        "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
+                        "measured_bytes_per_launch": m.get("bytes_per_launch") if isinstance(m, dict) else None}
+        return out
+
+
 def max_over_ranks(elapsed: float, device: torch.device) -> float:
     """The job's wall time: the slowest rank's timed region (all ranks get the same value)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
@@ -208,6 +311,10 @@ def main():
     timed(step, max(2, min(args.steps, 10)))
     probe.disable()
     ps = probe.summary()
+    # the HBM-bound kernels (BN backward passes, gate backward, upsample backward, materialised pool /
+    # upsample, first conv, 1x1 convs): algorithmic bytes / HIP-event time, in a separate pass
+    with HbmProbe() as hp:
+        timed(step, 2)
 
     # SURVEY §8(d) also asks for the rate without the optimizer: the same fwd + loss + bwd (+ gradient
     # averaging) micro-steps, gradients dropped instead of clip + AdamW (reported beside `value`)
@@ -228,10 +335,11 @@ def main():
     peak = MFMA_PEAK_TFLOPS[args.precision]
     achieved = ps["tflops"] or 0.0
     traffic = None
+    tr = {}
     tfile = ROOT / "profiles" / "traffic.json"
     if tfile.exists():
         tr = json.loads(tfile.read_text())
-        ent = tr.get(target)
+        ent = tr.get(f"{target}@{args.size}x{args.in_ch}") or tr.get(target)
         traffic = ent.get("bytes_per_launch") if isinstance(ent, dict) else ent
     headline = (args.size, args.in_ch, args.accum) == (512, 1, 1)
     metric = METRIC if headline else (
@@ -258,6 +366,10 @@ def main():
                      "launches": ps["launches"], "avg_us": round(ps["avg_us"], 2) if ps["avg_us"] else None,
                      "flops_per_launch": round(ps["flops"] / ps["launches"]) if ps["launches"] else None,
                      "timed": "separate probe pass (HIP events on the launch stream), not the headline loop"},
+        "hbm": {"peak": HBM_PEAK_GBS, "unit": "GB/s", "kernels": hp.summary(tr),
+                "note": "algorithmic bytes (each operand read once, each output written once) / HIP-event time "
+                        "per launch, separate pass; measured_bytes_per_launch: rocprofv3 FETCH_SIZE x2 + "
+                        "WRITE_SIZE (profiles/traffic.json)"},
         "final_loss": round(float(loss.detach()), 5),
         "without_optimizer": {"value": round(world * args.batch * args.accum * args.steps / el_nb, 3),
                               "ms_per_step": round(el_nb / args.steps * 1e3, 3),

@@ -39,9 +39,26 @@ def seeded_init(kind: str, in_ch: int):
     return {k: v.clone() for k, v in make_model(kind, in_ch).state_dict().items()}
 
 
-def oracle_run(init, x, t, dev, dtype, kind="attention", training=True, autocast=None, want_eval=True):
-    """The oracle's fwd + DiceBCE + bwd with the parameters/buffers of `init` on `dev` in `dtype`.
-    autocast: None, or the 16-bit dtype of a torch.autocast region around the forward."""
+def linear_probe(shape, seed=77):
+    """fixed N(0,1) weights R for the linear loss L = mean(logits * R): dL/dlogits = R / numel exactly, so a
+    gradient comparison through the network is not dominated by the conditioning of the loss"""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g)
+
+
+def _loss(out, t, loss):
+    from oracle import unet_oracle as O
+    if isinstance(loss, str):
+        return O.dice_bce_loss(out, t)
+    r = loss.to(out.device, out.dtype)
+    return (out * r).sum() / out.numel()
+
+
+def oracle_run(init, x, t, dev, dtype, kind="attention", training=True, autocast=None, want_eval=True,
+               loss="dice_bce"):
+    """The oracle's fwd + loss + bwd with the parameters/buffers of `init` on `dev` in `dtype`.
+    autocast: None, or the 16-bit dtype of a torch.autocast region around the forward.  loss: "dice_bce"
+    (the reference's DiceBCELoss) or a tensor R (the linear loss mean(logits * R))."""
     from oracle import unet_oracle as O
     fwd = forward_fn(kind)
     p = {}
@@ -59,7 +76,7 @@ def oracle_run(init, x, t, dev, dtype, kind="attention", training=True, autocast
         out = out.float()
     else:
         out = fwd(p, xx, training=training)
-    loss = O.dice_bce_loss(out, t.to(dev))
+    loss = _loss(out, t.to(dev), loss)
     loss.backward()
     grads = {k: p[k].grad.detach().double().cpu() for k in init if p[k].requires_grad}
     bufs = {k: v.detach().cpu() for k, v in p.items() if "running" in k or "num_batches" in k}
@@ -106,9 +123,9 @@ def hip_model(init, prec, kind="attention", in_ch=1, training=True):
     return m
 
 
-def hip_run(init, x, t, prec, kind="attention", in_ch=1, training=True, log=None, env=None):
-    """HIP fwd + DiceBCE + bwd; `log` collects the (conv instantiation, output mode) pairs launched;
-    `env` temporarily sets environment switches (e.g. UNET_NO_BNB_FUSE)."""
+def hip_run(init, x, t, prec, kind="attention", in_ch=1, training=True, log=None, env=None, loss="dice_bce"):
+    """HIP fwd + loss (DiceBCE, or the linear loss of a tensor R) + bwd; `log` collects the (conv
+    instantiation, output mode) pairs launched; `env` temporarily sets environment switches."""
     from unet._hip.runtime import probe
     from unet.utils.loss import DiceBCELoss
     m = hip_model(init, prec, kind, in_ch, training)
@@ -117,8 +134,11 @@ def hip_run(init, x, t, prec, kind="attention", in_ch=1, training=True, log=None
     try:
         os.environ.update(env or {})
         out = m(x.cuda())
-        loss = DiceBCELoss()(out, t.cuda())
-        loss.backward()
+        if isinstance(loss, str):
+            lv = DiceBCELoss()(out, t.cuda())
+        else:
+            lv = (out * loss.cuda()).sum() / out.numel()
+        lv.backward()
         torch.cuda.synchronize()
     finally:
         probe.log = None
@@ -128,7 +148,7 @@ def hip_run(init, x, t, prec, kind="attention", in_ch=1, training=True, log=None
             else:
                 os.environ[k] = v
     grads = {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()}
-    return m, out.detach(), float(loss.detach()), grads
+    return m, out.detach(), float(lv.detach()), grads
 
 
 def rel_l2(a, b):

@@ -37,8 +37,20 @@ def _threads():
 
 
 def _conv_kinds(log):
-    """{instantiation name} of the 3x3 / 1x1 convs launched, split by family"""
-    names = {k for k, _ in log}
+    """{instantiation name} of the convs launched"""
+    return {k for k, _ in log}
+
+
+def _assert_16bit_paths(log, prec):
+    """every conv of a 16-bit run is on a 16-bit MFMA kernel (no generic fallback; conv2 only for the small-map
+    1x1 projections), and the large maps' 3x3 forward (mode 0) and dgrad (modes 0 / 1) ran on conv5
+    (csrc/conv5.hip, the bench's kernel)"""
+    names = _conv_kinds(log)
+    bad = [n for n in names if n.startswith(("conv_generic", "conv2_kernel<fp32")) or (n.startswith("conv2_kernel")
+                                                                                      and ",3," in n)]
+    assert not bad, sorted(names)
+    assert any(n.startswith(f"conv5_kernel<{prec},") and m == 0 for n, m in log), sorted(names)
+    assert any(n.startswith(f"conv5_kernel<{prec},") and m == 1 for n, m in log), sorted(names)
     return names
 
 
@@ -97,10 +109,7 @@ def test_c2_unet_bf16_vs_oracle(c2_ref):
     ref, f64, ac = c2_ref, c2_ref["f64"], c2_ref["ac16"]
     log = []
     m, out, loss, grads = hip_run(ref["init"], ref["x"], ref["t"], "bf16", kind="unet", log=log)
-    names = _conv_kinds(log)
-    assert "conv3_kernel<bf16,3,1,4,1,8,1>" in names and "conv3_kernel<bf16,3,1,4,2,8,1>" in names, sorted(names)
-    assert "conv3_kernel<bf16,3,2,4,2,8,1>" in names and "conv3_kernel<bf16,3,2,4,1,8,1>" in names, sorted(names)
-    assert not any(n.startswith(("conv2_kernel", "conv_generic")) for n in names), sorted(names)
+    _assert_16bit_paths(log, "bf16")
     print()
     e, agree, lrel, r = report16("C2 bf16 HIP     ", out, loss, grads, f64)
     e_a, agree_a, _, r_a = report16("C2 bf16 autocast", ac["out"], ac["loss"], ac["grads"], f64)
@@ -118,17 +127,21 @@ _EVAL_REFS = {}
 
 def _eval_ref(kind):
     if kind not in _EVAL_REFS:
+        from fullsize_common import linear_probe
         init = seeded_init(kind, 1)
         g = torch.Generator().manual_seed(2026 if kind == "unet" else 2024)
         x = torch.rand(N, 1, S, S, generator=g) * 2 - 1
         t = discs(N, S, S, g)
         init = batch_running_stats(init, x, kind)
-        _EVAL_REFS[kind] = {
-            "init": init, "x": x, "t": t,
-            "f64": oracle_run(init, x, t, "cuda", torch.float64, kind=kind, training=False, want_eval=False),
-            "ac": {dt: oracle_run(init, x, t, "cuda", torch.float32, kind=kind, training=False, autocast=dt,
-                                  want_eval=False) for dt in (torch.bfloat16, torch.float16)},
-        }
+        R = linear_probe((N, 2, S, S))
+        ref = {"init": init, "x": x, "t": t, "R": R}
+        for name, loss in (("dice_bce", "dice_bce"), ("linear", R)):
+            ref[name] = {
+                "f64": oracle_run(init, x, t, "cuda", torch.float64, kind=kind, training=False, want_eval=False,
+                                  loss=loss),
+                "ac": {dt: oracle_run(init, x, t, "cuda", torch.float32, kind=kind, training=False, autocast=dt,
+                                      want_eval=False, loss=loss) for dt in (torch.bfloat16, torch.float16)}}
+        _EVAL_REFS[kind] = ref
     return _EVAL_REFS[kind]
 
 
@@ -136,28 +149,37 @@ def _eval_ref(kind):
 @pytest.mark.parametrize("kind", ["unet", "attention"])
 def test_eval_mode_16bit_fwd_bwd_vs_fp64(kind, prec):
     """C2 / C3 network at full size in eval mode (running statistics = one batch's statistics), forward +
-    DiceBCE + backward through the 16-bit kernels (conv3 y and dgrad tiles incl. the fused BN-backward sums,
-    wgrad2, the gate kernels, the pooled BN backward) against the fp64 oracle: logits and all-parameter
-    gradient rel-L2 <= 2e-2."""
+    loss + backward through the 16-bit kernels (conv5 / conv3 y and dgrad tiles incl. the fused BN-backward
+    sums, wgrad2, the gate kernels, the pooled BN backward) against the fp64 oracle.
+    Gate (the discriminating one): with the linear loss mean(logits * R) — whose logit gradient is exactly R,
+    so the comparison measures the network's forward and backward, not the loss's conditioning — logits and
+    all-parameter gradient rel-L2 <= 2e-2 and no parameter tensor worse than 0.1.  With the reference's
+    DiceBCELoss the same eval-mode network is ill-conditioned (measured: autocast-bf16 gradients at 0.85,
+    autocast-fp16 at 0.99 rel-L2 vs fp64), so that leg is reported and gated only against autocast."""
     _threads()
     ref = _eval_ref(kind)
-    f64 = ref["f64"]
-    log = []
-    m, out, loss, grads = hip_run(ref["init"], ref["x"], ref["t"], prec, kind=kind, training=False, log=log)
-    names = _conv_kinds(log)
-    assert f"conv3_kernel<{prec},3,1,4,1,8,1>" in names and f"conv3_kernel<{prec},3,2,4,2,8,1>" in names, sorted(names)
-    ac = ref["ac"][torch.bfloat16 if prec == "bf16" else torch.float16]
-    print()
-    e, agree, lrel, r = report16(f"{kind} eval {prec} HIP     ", out, loss, grads, f64)
-    e_a, _, _, r_a = report16(f"{kind} eval {prec} autocast", ac["out"], ac["loss"], ac["grads"], f64)
+    dt = torch.bfloat16 if prec == "bf16" else torch.float16
+    res = {}
+    for name in ("dice_bce", "linear"):
+        f64, ac = ref[name]["f64"], ref[name]["ac"][dt]
+        log = []
+        loss = "dice_bce" if name == "dice_bce" else ref["R"]
+        m, out, lv, grads = hip_run(ref["init"], ref["x"], ref["t"], prec, kind=kind, training=False, log=log,
+                                    loss=loss)
+        _assert_16bit_paths(log, prec)
+        print()
+        e, agree, lrel, r = report16(f"{kind} eval {prec} {name:8s} HIP     ", out, lv, grads, f64)
+        e_a, _, _, r_a = report16(f"{kind} eval {prec} {name:8s} autocast", ac["out"], ac["loss"], ac["grads"], f64)
+        per = {k: rel_l2(grads[k], g) for k, g in f64["grads"].items() if float(g.norm()) > 0}
+        worst = max(per.items(), key=lambda kv: kv[1])
+        print(f"{kind} eval {prec} {name}: worst per-tensor gradient rel-L2 {worst[1]:.3e} ({worst[0]})")
+        res[name] = (e, r, e_a, r_a, worst)
+    e, r, e_a, r_a, worst = res["linear"]
     assert e <= 2e-2, (e, e_a)
     assert r <= 2e-2, (r, r_a)
-    assert lrel <= 2e-3, lrel
-    # per-layer: no single parameter's gradient far off (a mis-wired stage would be)
-    per = {k: rel_l2(grads[k], g) for k, g in f64["grads"].items() if float(g.norm()) > 0}
-    worst = max(per.items(), key=lambda kv: kv[1])
-    print(f"{kind} eval {prec}: worst per-tensor gradient rel-L2 {worst[1]:.3e} ({worst[0]})")
     assert worst[1] <= 0.1, worst
+    e, r, e_a, r_a, _ = res["dice_bce"]
+    assert e <= 1.1 * e_a + 5e-3 and r <= 1.1 * r_a + 2e-2, (e, e_a, r, r_a)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -195,15 +217,24 @@ def test_bnb_epilogue_fused_vs_unfused(prec, training):
         counts.append(n[0])
     (m0, o0, l0, g0), (m1, o1, l1, g1) = runs
     print(f"\nseparate BN-backward reductions: fused {counts[0]}, unfused {counts[1]}")
-    assert counts[1] - counts[0] >= 2, counts          # inc / up4 (64-channel middle maps at 256^2) fuse
+    assert counts[1] - counts[0] >= 2, counts          # the large maps' middle BNs fuse (conv5 / conv3 tiles)
     assert torch.equal(o0, o1) and l0 == l1
     bn_keys = [k for k in g0 if ".double_conv.1." in k]
     worst_bn = max(float((g0[k] - g1[k]).abs().max()) / (float(g1[k].abs().max()) + 1e-30) for k in bn_keys)
     w, k, r = grad_errs(g0, g1)
     print(f"{prec} {'train' if training else 'eval'}: middle-BN grads worst max-norm diff {worst_bn:.2e}; all params "
           f"rel-L2 {r:.2e}, worst {w:.2e} ({k})")
-    assert worst_bn <= 2e-3, worst_bn
-    assert r <= 1e-2, (r, k)
+    # the first backward stage that uses the fused sums (up4's middle BN) sees identical inputs on both paths:
+    # only the summation order differs.  Everything after it inherits a few flipped 16-bit roundings of dy, which
+    # train-mode BN (batch statistics) amplifies stage by stage; in eval mode nothing amplifies them.
+    k4 = "up4.conv.double_conv.1.weight"
+    first = float((g0[k4] - g1[k4]).abs().max()) / float(g1[k4].abs().max())
+    print(f"first fused stage ({k4}) max-norm diff {first:.2e}")
+    assert first <= 1e-5, first
+    if training:
+        assert worst_bn <= 5e-2 and r <= 2e-2, (worst_bn, r, k)
+    else:
+        assert worst_bn <= 1e-5 and r <= 1e-6, (worst_bn, r, k)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -227,10 +258,8 @@ def test_c5_fp16_1024_vs_oracle(c5_ref):
     ref, f64, ac = c5_ref, c5_ref["f64"], c5_ref["ac16"]
     log = []
     m, out, loss, grads = hip_run(ref["init"], ref["x"], ref["t"], "fp16", in_ch=3, log=log)
-    names = _conv_kinds(log)
-    for k in ("conv3_kernel<fp16,3,1,4,1,8,1>", "conv3_kernel<fp16,3,1,4,2,8,1>", "conv3_kernel<fp16,3,2,4,2,8,1>",
-              "conv3_kernel<fp16,3,2,4,1,8,1>", "smallcin_fwd_kernel<fp16>"):
-        assert k in names, (k, sorted(names))
+    names = _assert_16bit_paths(log, "fp16")
+    assert "smallcin_fwd_kernel<fp16>" in names, sorted(names)
     print()
     e, agree, lrel, r = report16("C5 fp16 HIP     ", out, loss, grads, f64)
     e_a, agree_a, _, r_a = report16("C5 fp16 autocast", ac["out"], ac["loss"], ac["grads"], f64)

@@ -1,5 +1,6 @@
-"""conv4 (csrc/conv4.hip: the 3x3 conv on v_mfma_f32_32x32x16) against torch fp32 on the same 16-bit operands,
-for every epilogue and source kind it serves, at bench sizes (the persistent multi-tile loop runs) and with
+"""conv5 (csrc/conv5.hip: the LDS-DMA 3x3 conv on v_mfma_f32_32x32x16, the default path on large maps) and
+conv4 (csrc/conv4.hip: the register-staged 32x32x16 kernel, UNET_CONV5=0 UNET_CONV4=1) against torch fp32 on
+the same 16-bit operands, for every epilogue and source kind they serve, at bench sizes (the persistent multi-tile loop runs) and with
 partial tiles in both directions.  Reference ops: nn.Conv2d(k=3, pad=1, bias=False) forward
 (unet/models/layers.py:32,35) and its input gradient; BatchNorm2d forward partial sums / backward sums of
 the DoubleConv (layers.py:33,36).  Gates as the conv3 bench-tile tests: rel-L2 <= 4e-3, max-abs <= 2e-2 (1 +
@@ -17,19 +18,26 @@ Y_SHAPES = [(4, 512, 512, 64, 64), (4, 256, 256, 64, 128), (4, 256, 256, 128, 12
             (3, 200, 328, 64, 128), (8, 258, 98, 96, 64)]
 
 
-def _want(prec, cout):
+PATH = {"conv5": {"UNET_CONV5": "1", "UNET_CONV4": "0"}, "conv4": {"UNET_CONV5": "0", "UNET_CONV4": "1"}}
+
+
+def _want(prec, cout, path):
+    if path == "conv5":
+        return f"conv5_kernel<{TN[prec]},4>"
     return f"conv4_kernel<{TN[prec]},4,2,1,4>" if cout <= 64 else f"conv4_kernel<{TN[prec]},2,4,1,4>"
 
 
-@pytest.fixture(autouse=True)
-def _conv4_on(monkeypatch):
-    monkeypatch.setenv("UNET_CONV4", "1")
+@pytest.fixture(params=["conv5", "conv4"])
+def path(request, monkeypatch):
+    for k, v in PATH[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
 
 
 @pytest.mark.parametrize("shape", Y_SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("src", ["plain", "act", "act_gate", "concat"])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv4_y_stats(prec, src, shape):
+def test_conv4_y_stats(prec, src, shape, path):
     L, R = _lib(), _rt()
     N, H, W, cin, cout = shape
     dt = DT[prec]
@@ -69,7 +77,7 @@ def test_conv4_y_stats(prec, src, shape):
     st = torch.full((2, cout, rows), float("nan"), device="cuda")
     out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
     d = _conv(prec, srcs, N, H, W, cin, w, 3, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
-    assert _variant(d) == _want(prec, cout), _variant(d)
+    assert _variant(d) == _want(prec, cout, path), _variant(d)
     ref = F.conv2d(x.permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
     _close_bf16(out.float(), ref, "y")
     r = ref.double().reshape(-1, cout)
@@ -85,7 +93,7 @@ DGRAD_SHAPES = [(4, 512, 512, 128, 64), (4, 512, 512, 64, 64), (4, 256, 256, 256
 
 @pytest.mark.parametrize("shape", DGRAD_SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv4_dgrad_f32_split_accum(prec, shape):
+def test_conv4_dgrad_f32_split_accum(prec, shape, path):
     """dgrad of a forward conv cin -> cout: dy[cout] -> dx[cin], fp32, split across the concat with the first
     part accumulated (UNET_OUT_F32)."""
     L = _lib()
@@ -102,7 +110,7 @@ def test_conv4_dgrad_f32_split_accum(prec, shape):
     o2 = torch.full((N, H, W, cin - split), float("nan"), device="cuda")
     d = _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
               split=split, accum=1, accum2=0)
-    assert _variant(d) == _want(prec, cin), _variant(d)
+    assert _variant(d) == _want(prec, cin, path), _variant(d)
     _close_bf16(torch.cat([o1 - 0.5, o2], -1), ref, "dgrad f32")
     # unsplit, stored
     o = torch.full((N, H, W, cin), float("nan"), device="cuda")
@@ -111,8 +119,8 @@ def test_conv4_dgrad_f32_split_accum(prec, shape):
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv4_matches_conv3(prec, monkeypatch):
-    """The two 3x3 kernels on the same inputs agree to fp32 summation-order noise before rounding."""
+def test_conv4_matches_conv3(prec, path, monkeypatch):
+    """The 32x32x16 kernels and conv3 on the same inputs agree to fp32 summation-order noise."""
     L = _lib()
     N, H, W, cin, cout = 4, 256, 256, 128, 128
     dt = DT[prec]
@@ -121,13 +129,14 @@ def test_conv4_matches_conv3(prec, monkeypatch):
     w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
     outs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("UNET_CONV4", flag)
+        for k, v in PATH[path].items():
+            monkeypatch.setenv(k, v if flag == "1" else "0")
         o = torch.full((N, H, W, cout), float("nan"), device="cuda")
         src = L.Src()
         src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, y.data_ptr()
         d = _conv(prec, [src], N, H, W, cin, w, 3, L.OUT_F32, transpose=True, out=o.data_ptr(), split=cin)
         outs.append((_variant(d), o))
     (v4, o4), (v3, o3) = outs
-    assert v4.startswith("conv4_kernel") and v3.startswith("conv3_kernel"), (v4, v3)
+    assert v4.startswith(f"{path}_kernel") and v3.startswith("conv3_kernel"), (v4, v3)
     rel = float((o4 - o3).double().norm() / o3.double().norm())
     assert rel <= 1e-5, rel

@@ -2,9 +2,9 @@
 batch 4 x 1 x 512 x 512, train-mode forward + DiceBCE + backward (reference unet.py:175-211,
 loss.py:153-191), HIP path vs the CPU oracle on the same seeded weights and inputs.
 
-At this size the dispatcher picks the same kernel instantiations as `bench.py` (the 4-wave w4 y-epilogue
-conv3 tiles, the 8-wave MI=8 dgrad and pool-routing tiles, the persistent multi-tile loop, wgrad2 with
->32 split-K slabs, the pointwise gate kernels); the bf16 test asserts that they ran.
+At this size the dispatcher picks the same kernel instantiations as `bench.py` (conv5 on the large maps, the
+conv3 tiles on the 32^2 / 64^2 ones, the persistent multi-tile loops, wgrad2 with >32 split-K slabs, the
+pointwise gate kernels); the 16-bit tests assert that no fallback kernel ran and that conv5 did.
 
 Gates:
   fp32 operand mode, against the CPU fp32 oracle (the reference's own execution) — logits within 1e-4
@@ -161,15 +161,6 @@ def test_fullsize_fp32_vs_oracle(full_ref):
     assert ee <= 1e-4 * (1 + float(c32["eval"].abs().max())), ee
 
 
-BENCH_CONV3 = {  # (instantiation, output mode) that bench.py's step launches (csrc/conv.hip pick_cfg)
-    ("conv3_kernel<bf16,3,1,4,1,8,1>", 0),   # w4 y epilogue, 64 channels (inc.3, up4.conv.3, dgrad -> middle)
-    ("conv3_kernel<bf16,3,1,4,2,8,1>", 0),   # w4 y epilogue, 128 channels
-    ("conv3_kernel<bf16,3,2,4,2,8,1>", 1),   # MI=8 fp32 dgrad (split over the concat; the Down blocks'
-                                             # pooled-resolution dgrads, routed by the BN backward)
-    ("conv3_kernel<bf16,3,2,4,1,8,1>", 1),   # MI=8 fp32 dgrad, 64 channels (down1 -> inc, pooled)
-}
-
-
 def _bf16_report(name, out, loss, grads, f64):
     e = rel_err(out, f64["out"])
     agree = float((out.double().cpu().argmax(1) == f64["out"].argmax(1)).double().mean())
@@ -194,9 +185,8 @@ def test_fullsize_16bit_vs_oracle(full_ref, prec):
                                                          autocast=torch.float16)
     log = []
     m, out, loss = _run(ref, prec, log)
-    ran = set(log)
-    missing = {(k.replace("bf16", prec), mode) for k, mode in BENCH_CONV3} - ran
-    assert not missing, (missing, sorted(ran))
+    from test_gpu_configs import _assert_16bit_paths
+    _assert_16bit_paths(log, prec)
     grads = {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()}
     print()
     e, agree, lrel, r = _bf16_report(f"{prec} HIP      ", out, loss, grads, f64)

@@ -483,6 +483,10 @@ static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t s
 #include "conv3_body.inc"
 
 template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
+bool conv5_eligible(const unet_conv_desc* d);   // conv5.hip: the LDS-DMA 3x3 path
+int conv5_run(const unet_conv_desc* d, hipStream_t st);
+int conv5_stats_rows(const unet_conv_desc* d);
+int conv5_variant(const unet_conv_desc* d, char* buf, int len);
 bool conv4_eligible(const unet_conv_desc* d);   // conv4.hip: the 32x32x16-MFMA 3x3 path
 int conv4_run(const unet_conv_desc* d, hipStream_t st);
 int conv4_stats_rows(const unet_conv_desc* d);
@@ -512,6 +516,7 @@ template <typename T>
 static int dispatch_conv(const unet_conv_desc* d, hipStream_t st) {
   if (!fast_eligible(d)) return dispatch_generic<T>(d, st);
   if constexpr (sizeof(T) == 2) {
+    if (conv5_eligible(d)) return conv5_run(d, st);
     if (conv4_eligible(d)) return conv4_run(d, st);
   }
   const ConvCfg c = pick_cfg(d);
@@ -600,7 +605,7 @@ int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8)
 // does unet_conv reduce d's bnb_* sums in the conv epilogue (rows = the conv's M tiles)?
 static bool bnb_in_epilogue(const unet_conv_desc* d) {
   if (smallcin_conv_ok(d) || pw_conv_ok(d) || !fast_eligible(d) || d->dtype == UNET_F32) return false;
-  if (conv4_eligible(d)) return true;
+  if (conv5_eligible(d) || conv4_eligible(d)) return true;
   return conv3_bnb_tile(d, pick_cfg(d));
 }
 
@@ -609,6 +614,7 @@ int unet_conv_stats_rows(const unet_conv_desc* d) {
   if (smallcin_conv_ok(d)) return smallcin_rows((long long)d->N * d->H * d->W);
   if (pw_conv_ok(d)) return pw_conv_rows(d);
   if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
+  if (conv5_eligible(d)) return conv5_stats_rows(d);
   if (conv4_eligible(d)) return conv4_stats_rows(d);
   const ConvCfg c = pick_cfg(d);
   return d->N * cdiv(d->W, CTW) * cdiv(d->H, 4 * c.wm);
@@ -625,6 +631,7 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
              d->Cout <= 32 ? 32 : 64);
     return 0;
   }
+  if (conv5_eligible(d)) return conv5_variant(d, buf, len);
   if (conv4_eligible(d)) return conv4_variant(d, buf, len);
   const ConvCfg c = pick_cfg(d);
   if (conv3_eligible(d)) {

@@ -23,42 +23,23 @@
 //    in place: the 32x16 A fragment of channels co..co+31, k-half s of a 32-channel chunk is four 256-byte
 //    runs of it (lane-constant offset), prefetched two taps ahead into a 3-slot VGPR ring; no repacking.
 //  * Persistent over M tiles with the next tile's chunk 0 staged under the last chunk, as conv3.
-//  * Epilogues: y (16-bit) + per-(tile, wave) BatchNorm partial sums; y + the BatchNorm-backward sums of the
-//    activation it is the gradient of (unet_conv_desc.bnb_*); fp32 gradient (concat split, accumulate).
-#include "conv_src16.h"
+//  * Epilogues: y (16-bit) + BatchNorm partial sums; y + the BatchNorm-backward sums of the activation it is
+//    the gradient of (unet_conv_desc.bnb_*); fp32 gradient (concat split, accumulate).  The sums are kept per
+//    lane across all the tiles a workgroup visits (2 VALU per value per tile) and reduced across lanes once,
+//    at the end: one partial row per wave of the persistent grid, so the finalize kernels read ~1k rows
+//    instead of one per tile.
+#include "conv_mfma32.h"
 
 namespace unet {
-
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-
-template <typename T> struct Mma32;
-template <> struct Mma32<bf16> {
-  typedef bf16x8 frag;
-  __device__ static __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-  }
-};
-template <> struct Mma32<f16> {
-  typedef f16x8 frag;
-  __device__ static __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-  }
-};
 
 constexpr int C4W = 32;          // tile width in pixels (the MFMA's N)
 constexpr int C4_NPAD = 128;     // packed weight rows are padded to this (conv.hip PACK_NPAD)
 constexpr int OM4_Y = 0, OM4_F32 = 1, OM4_BNB = 2;
 
-// sum over the 32 lanes l with equal l >> 5 (one pixel row of the accumulator): DPP row sums, then the
-// partner row through v_permlane16_swap; every lane receives its half's total
-__device__ __forceinline__ float half32_sum(float v) {
-  v = row16_sum(v);
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
 // wave tile: MI rows x 32 px x (32*NJ) channels; block: WM x WN waves -> (MI*WM) rows x 32 px x (32*NJ*WN) ch.
-template <typename T, int WM, int WN, int NJ, int MI, int OM, int SK>
+// ABL (diagnostic ablations, unet_diag_conv4_ablate; 0 in the product): 1 no next-chunk halo staging, 2 no
+// weight loads inside the chunk loop, 4 no epilogue stores / sums, 8 no per-chunk barrier
+template <typename T, int WM, int WN, int NJ, int MI, int OM, int SK, int ABL = 0>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_kernel(const unet_conv_desc d, int tiles_w,
                                                                                    int tiles_h, int mtiles, int nch16) {
   using F = typename Mma32<T>::frag;
@@ -127,6 +108,16 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
   for (int j = 0; j < NJ; ++j) { B[0][j] = afrag(j, 0, tap_of(0)); B[1][j] = afrag(j, 0, tap_of(1)); }
   __syncthreads();
 
+  // BatchNorm sums (y: Σy, Σy²; BNB: Σg, Σg·y1) of this lane's pixel column and 16*NJ channels, accumulated
+  // over every tile the workgroup visits and reduced across lanes / written once at the end (one partial
+  // row per wave: [2][Cout][gridDim.x * WM] for y, [2][gridDim.x * WM][Cout] for BNB)
+  constexpr bool SUMS = OM == OM4_Y || OM == OM4_BNB;
+  float sA[SUMS ? NJ : 1][16], sB[SUMS ? NJ : 1][16];
+#pragma unroll
+  for (int j = 0; j < (SUMS ? NJ : 1); ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { sA[j][r] = 0.f; sB[j][r] = 0.f; }
+
   int buf = 0;
   for (;;) {
     const int mt_next = mt + (int)gridDim.x;
@@ -164,7 +155,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
 #pragma unroll
       for (int st = 0; st < 9; ++st) {
         const int dx = st / 3, dy = st % 3;
-        {
+        if constexpr (!(ABL & 2)) {
           const int s2 = st + 2;
           if (s2 < 9) {
 #pragma unroll
@@ -174,7 +165,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
             for (int j = 0; j < NJ; ++j) B[s2 % 3][j] = afrag(j, cw, tap_of(s2 - 9));
           }
         }
-        if (st < 3 && has_next) {
+        if (st < 3 && has_next && !(ABL & 1)) {
 #pragma unroll
           for (int u = 0; u < IPT; ++u)
             if (st * IPT + u < ITEMS) conv3_issue<1, SK>(cv, geo[st * IPT + u], q[st * IPT + u]);
@@ -190,7 +181,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
 #pragma unroll
           for (int i = 0; i < MI; ++i) acc[i][j] = Mma32<T>::mma(a, xr[i + dy], acc[i][j]);
         }
-        if (st >= 6 && has_next) {
+        if (st >= 6 && has_next && !(ABL & 1)) {
 #pragma unroll
           for (int u = 0; u < IPT; ++u) {
             const int k = (st - 6) * IPT + u;
@@ -203,12 +194,19 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
         }
         if (dy == 2) __builtin_amdgcn_sched_barrier(0);
       }
-      __syncthreads();
+      if constexpr (!(ABL & 8)) __syncthreads();
       buf ^= 1;
     }
 
     // ---------------- epilogue ----------------
-    {
+    if constexpr (ABL & 4) {
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) sum += acc[i][j][0] + acc[i][j][5] + acc[i][j][10] + acc[i][j][15];
+      if (sum == 12345.f) ((float*)d.out)[tid] = sum;
+    } else {
       const int px = lane & 31, hh = lane >> 5;
       const int ow = w0 + px;
       const bool colok = ow < d.W;
@@ -216,8 +214,6 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
       int rows = d.H - oh0;
       rows = rows < 0 ? 0 : (rows > MI ? MI : rows);
       const unsigned pix0 = ((unsigned)n * d.H + oh0) * (unsigned)d.W + ow;   // < 2^30 (conv4_eligible)
-      const int srow = mt * WM + wm;               // partial-sum row of this wave
-      const int srows = mtiles * WM;
       if constexpr (OM == OM4_Y) {
         T* y = (T*)d.out;
 #pragma unroll
@@ -238,33 +234,21 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
             }
         }
         if (d.stats) {
-          // BatchNorm partial sums [2][Cout][srows] of the fp32 accumulators: over the wave's rows in
-          // registers, then over the 32 pixels of a half-wave
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              float a = 0.f, b = 0.f;
+            for (int r = 0; r < 16; ++r)
 #pragma unroll
               for (int i = 0; i < MI; ++i) {
                 const float x = (colok && i < rows) ? acc[i][j][r] : 0.f;
-                a += x;
-                b = __builtin_fmaf(x, x, b);
+                sA[j][r] += x;
+                sB[j][r] = __builtin_fmaf(x, x, sB[j][r]);
               }
-              a = half32_sum(a);
-              b = half32_sum(b);
-              const int co = cw0 + 32 * j + 8 * (r >> 2) + 4 * hh + (r & 3);
-              if (px == 0 && co < d.Cout) {
-                d.stats[(size_t)co * srows + srow] = a;
-                d.stats[((size_t)d.Cout + co) * srows + srow] = b;
-              }
-            }
         }
       } else if constexpr (OM == OM4_BNB) {
         // y (the gradient of a single-consumer activation, 16-bit) + that activation's BatchNorm backward
-        // sums: g = the value as stored where relu?(y1 * scale + shift) > 0; per channel Σg and
-        // Σg·(y1 - mean)·invstd = invstd·(Σg·y1 - mean·Σg) (formed once per channel, after the lane sums);
-        // layout bnb_stats[2][srows][Cout]
+        // sums: g = the value as stored where relu?(y1 * scale + shift) > 0; Σg and Σg·y1 per lane here,
+        // Σg·(y1 - mean)·invstd = invstd·(Σg·y1 - mean·Σg) formed once per channel at the end
         T* y = (T*)d.out;
         const T* y1 = (const T*)d.bnb_y;
         uint2 yv[MI][NJ][4];
@@ -286,18 +270,12 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
             const int co = cw0 + 32 * j + 8 * g + 4 * hh;
             const bool cok = co < d.Cout;
             float sc4[4] = {0.f, 0.f, 0.f, 0.f}, sf4[4] = {0.f, 0.f, 0.f, 0.f};
-            float mu4[4] = {0.f, 0.f, 0.f, 0.f}, is4[4] = {0.f, 0.f, 0.f, 0.f};
-            if (cok) {
+            if (cok && d.bnb_relu) {
               const float4 a4 = *reinterpret_cast<const float4*>(d.bnb_scale + co);
               const float4 b4 = *reinterpret_cast<const float4*>(d.bnb_shift + co);
-              const float4 m4 = *reinterpret_cast<const float4*>(d.bnb_mean + co);
-              const float4 i4 = *reinterpret_cast<const float4*>(d.bnb_invstd + co);
               sc4[0] = a4.x; sc4[1] = a4.y; sc4[2] = a4.z; sc4[3] = a4.w;
               sf4[0] = b4.x; sf4[1] = b4.y; sf4[2] = b4.z; sf4[3] = b4.w;
-              mu4[0] = m4.x; mu4[1] = m4.y; mu4[2] = m4.z; mu4[3] = m4.w;
-              is4[0] = i4.x; is4[1] = i4.y; is4[2] = i4.z; is4[3] = i4.w;
             }
-            float sa[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < MI; ++i) {
               const unsigned pix = pix0 + (unsigned)i * d.W;
@@ -305,29 +283,18 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
               uint2 pk;
               pk.x = pack2_16<T>(acc[i][j][4 * g], acc[i][j][4 * g + 1]);
               pk.y = pack2_16<T>(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
-              if (ok) *reinterpret_cast<uint2*>(y + (size_t)pix * d.Cout + co) = pk;
               if (ok) {
+                *reinterpret_cast<uint2*>(y + (size_t)pix * d.Cout + co) = pk;
                 float gv[4], yy[4];
                 unpack4_16<T>(pk, gv);
                 unpack4_16<T>(yv[i][j][g], yy);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   const float gg = (d.bnb_relu && !(yy[r] * sc4[r] + sf4[r] > 0.f)) ? 0.f : gv[r];
-                  sa[r] += gg;
-                  sb[r] = __builtin_fmaf(gg, yy[r], sb[r]);
+                  sA[j][4 * g + r] += gg;
+                  sB[j][4 * g + r] = __builtin_fmaf(gg, yy[r], sB[j][4 * g + r]);
                 }
               }
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              sa[r] = half32_sum(sa[r]);
-              sb[r] = half32_sum(sb[r]);
-              sb[r] = is4[r] * (sb[r] - mu4[r] * sa[r]);
-            }
-            if (px == 0 && cok) {
-              *reinterpret_cast<float4*>(d.bnb_stats + (size_t)srow * d.Cout + co) = make_float4(sa[0], sa[1], sa[2], sa[3]);
-              *reinterpret_cast<float4*>(d.bnb_stats + ((size_t)srows + srow) * d.Cout + co) =
-                  make_float4(sb[0], sb[1], sb[2], sb[3]);
             }
           }
       } else {  // OM4_F32: fp32 gradient, channels [0, split) -> out, [split, Cout) -> out2, optionally accumulated
@@ -380,6 +347,50 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN <= 4) ? 2 : 1) void conv4_ke
 #pragma unroll
     for (int j = 0; j < NJ; ++j) { B[0][j] = afrag(j, 0, tap_of(0)); B[1][j] = afrag(j, 0, tap_of(1)); }
   }
+
+  // ---- the workgroup's BatchNorm sums: over the 32 pixel columns of each half-wave, one row per wave ----
+  if constexpr (SUMS) {
+    const int hh = lane >> 5;
+    const int srow = blockIdx.x * WM + wm, srows = gridDim.x * WM;
+    if constexpr (OM == OM4_Y) {
+      if (d.stats) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float a = half32_sum(sA[j][r]), b = half32_sum(sB[j][r]);
+            const int co = cw0 + 32 * j + 8 * (r >> 2) + 4 * hh + (r & 3);
+            if ((lane & 31) == 0 && co < d.Cout) {
+              d.stats[(size_t)co * srows + srow] = a;
+              d.stats[((size_t)d.Cout + co) * srows + srow] = b;
+            }
+          }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int co = cw0 + 32 * j + 8 * g + 4 * hh;
+          float a[4], b[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            a[r] = half32_sum(sA[j][4 * g + r]);
+            b[r] = half32_sum(sB[j][4 * g + r]);
+          }
+          if ((lane & 31) == 0 && co < d.Cout) {
+            const float4 m4 = *reinterpret_cast<const float4*>(d.bnb_mean + co);
+            const float4 i4 = *reinterpret_cast<const float4*>(d.bnb_invstd + co);
+            const float mu[4] = {m4.x, m4.y, m4.z, m4.w}, is[4] = {i4.x, i4.y, i4.z, i4.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) b[r] = is[r] * (b[r] - mu[r] * a[r]);
+            *reinterpret_cast<float4*>(d.bnb_stats + (size_t)srow * d.Cout + co) = make_float4(a[0], a[1], a[2], a[3]);
+            *reinterpret_cast<float4*>(d.bnb_stats + ((size_t)srows + srow) * d.Cout + co) =
+                make_float4(b[0], b[1], b[2], b[3]);
+          }
+        }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -389,10 +400,11 @@ struct Cfg4 {
   int wm, wn, nj, mi;
 };
 
-// UNET_CONV4=0 routes these convs back to conv3 (A/B switch; read per call so tests can flip it)
+// UNET_CONV4=1 routes the eligible convs to conv4 (off by default until it beats conv3 on every layer it
+// takes; read per call so tests can flip it)
 static bool conv4_enabled() {
   const char* e = getenv("UNET_CONV4");
-  return !(e && atoi(e) == 0);
+  return e && atoi(e) != 0;
 }
 
 static Cfg4 conv4_cfg(const unet_conv_desc* d) {
@@ -425,9 +437,20 @@ bool conv4_eligible(const unet_conv_desc* d) {
   return work >= 512;
 }
 
+// persistent grid: about two (4-wave) workgroups per CU or one 8-wave workgroup, never more than the tiles
+static int conv4_gx(const unet_conv_desc* d, const Cfg4& c) {
+  const long long mt = conv4_mtiles(d, c);
+  const int gy = cdiv(d->Cout, 32 * c.nj * c.wn);
+  long long gx = cdiv(c.wm * c.wn <= 4 ? 512 : 256, gy);
+  if (gx > mt) gx = mt;
+  if (gx < 1) gx = 1;
+  return (int)gx;
+}
+
+// partial-sum rows: one per wave row of the persistent grid (conv4_kernel's SUMS)
 int conv4_stats_rows(const unet_conv_desc* d) {
   const Cfg4 c = conv4_cfg(d);
-  return (int)conv4_mtiles(d, c) * c.wm;
+  return conv4_gx(d, c) * c.wm;
 }
 
 int conv4_variant(const unet_conv_desc* d, char* buf, int len) {
@@ -436,16 +459,14 @@ int conv4_variant(const unet_conv_desc* d, char* buf, int len) {
   return 0;
 }
 
-template <typename T, int WM, int WN, int NJ, int MI, int OM, int SK>
+template <typename T, int WM, int WN, int NJ, int MI, int OM, int SK, int ABL = 0>
 static int launch4(const unet_conv_desc* d, hipStream_t st) {
   constexpr int TH = MI * WM, BN = WN * NJ * 32;
   const int tw = cdiv(d->W, C4W), th = cdiv(d->H, TH);
   const int mt = d->N * tw * th;
   const int gy = cdiv(d->Cout, BN);
-  int gx = cdiv(WM * WN <= 4 ? 512 : 256, gy);   // about two (4-wave) workgroups per CU, persistent
-  if (gx > mt) gx = mt;
-  if (gx < 1) gx = 1;
-  hipLaunchKernelGGL((conv4_kernel<T, WM, WN, NJ, MI, OM, SK>), dim3(gx, gy), dim3(64 * WM * WN), 0, st, *d, tw, th, mt,
+  const int gx = conv4_gx(d, Cfg4{WM, WN, NJ, MI});
+  hipLaunchKernelGGL((conv4_kernel<T, WM, WN, NJ, MI, OM, SK, ABL>), dim3(gx, gy), dim3(64 * WM * WN), 0, st, *d, tw, th, mt,
                      cdiv(d->Cin, 16));
   return check_launch("conv4");
 }
@@ -480,4 +501,33 @@ int conv4_run(const unet_conv_desc* d, hipStream_t st) {
   return d->dtype == UNET_F16 ? dispatch4<f16>(d, st) : dispatch4<bf16>(d, st);
 }
 
+template <int SK, int ABL>
+static int abl4(const unet_conv_desc* d, hipStream_t st) {
+  if (d->Cout <= 64) return launch4<bf16, 4, 2, 1, 4, OM4_Y, SK, ABL>(d, st);
+  return launch4<bf16, 2, 4, 1, 4, OM4_Y, SK, ABL>(d, st);
+}
+template <int SK>
+static int abl4_modes(const unet_conv_desc* d, int abl, hipStream_t st) {
+  switch (abl) {
+    case 0: return abl4<SK, 0>(d, st);
+    case 1: return abl4<SK, 1>(d, st);
+    case 2: return abl4<SK, 2>(d, st);
+    case 3: return abl4<SK, 3>(d, st);
+    case 4: return abl4<SK, 4>(d, st);
+    case 8: return abl4<SK, 8>(d, st);
+    case 7: return abl4<SK, 7>(d, st);
+    case 15: return abl4<SK, 15>(d, st);
+  }
+  return UNET_ERR_ARG;
+}
+
 }  // namespace unet
+
+// diagnostic (not part of the C ABI header): conv4 ablations of the bf16 y-mode kernel (ABL bits above) on
+// a one-source plain or BN-activation descriptor; tools/conv_ablate.py
+extern "C" int unet_diag_conv4_ablate(const unet_conv_desc* d, int abl, void* stream) {
+  using namespace unet;
+  if (!conv4_eligible(d) || d->nsrc != 1 || d->out_mode != UNET_OUT_Y || d->dtype != UNET_BF16) return UNET_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return d->src[0].kind == UNET_SRC_PLAIN ? abl4_modes<SK_PLAIN>(d, abl, st) : abl4_modes<SK_ACT>(d, abl, st);
+}

@@ -1,0 +1,613 @@
+// conv5.hip — 3x3 convolution (forward and dgrad) for gfx950 with an LDS-DMA operand pipeline.
+//
+// Replaces nn.Conv2d(k=3, pad=1, bias=False) of unet/models/layers.py:32,35 (every DoubleConv half) and the
+// input-gradient half of its convolution_backward, on maps large enough to fill the chip.
+//
+// Why: the register-staged kernels (conv3, conv4) spend most of their time waiting, not computing.  The
+// conv4 ablations (tools/conv4_ablate.py, 64->64 @ 4x512^2): 142 us full; 54 us with the halo staging, the
+// in-loop weight loads and the epilogue removed, i.e. the MFMA + LDS loop alone runs at 57 % of the bf16 peak.
+// The halo staging cost 39 us: its loads were issued 6 taps (~0.6 us) before use, less than the load
+// latency under full-chip streaming, and held registers while in flight.  Here every operand reaches LDS by
+// buffer_load ... lds (LDS DMA: no VGPRs, no VALU), issued TWO 16-channel chunks ahead:
+//  * input halo of chunk g+2: (TH+2) x 34 pixels x 16 channels, 16-byte slots in lane order; a plain source
+//    (dgrad dy, materialised pool / upsample) lands directly in the compute image (3-deep ring); a BN
+//    activation (+ attention gate) source lands in a raw ring and is transformed slot for slot by the lane
+//    that loaded it (BN-apply, ReLU, gate, zero padding) one chunk ahead — only that lane's vmcnt orders it,
+//    no barrier; scale / shift come from an LDS table, the gate pre-activation from per-lane DMA slots;
+//  * weights of chunk g+2: the 18 KB of 32x16 A fragments of the block's 64 output channels x 9 taps, read
+//    from conv3's fragment-major packing by per-lane addresses into a 3-deep ring (one 1 KB fragment per
+//    DMA instruction, ds_read_b128 in lane order: conflict free) — shared by the block's 8 waves instead of
+//    8 L2 streams;
+//  * one hand-counted s_waitcnt vmcnt(D) per chunk (D = this wave's DMAs for chunk g+2) and one raw
+//    s_barrier per chunk; no ordinary global load inside the chunk loop (hipcc would drain the DMA queue
+//    with vmcnt(0) in front of its first use).
+// The compute image is swizzled ((pixel >> 3) & 1 flips the two 16-byte channel halves of a pixel), which
+// makes the B-fragment ds_read_b128 (32 pixels x 2 halves per wave) bank-conflict free for every row and tap
+// (brute-force checked over the lane groups of MI355X_MICROARCH.md's LDS table).
+//
+// Tile: 16 rows x 32 px x 64 output channels per workgroup of 8 waves (4 row groups x 2 channel halves);
+// wave tile MI=4 rows x 32 px x 32 channels on v_mfma_f32_32x32x16 (D[co][px] = W[co][k] X[k][px]),
+// persistent over M tiles.  Epilogues as conv4: y (16-bit) + BatchNorm partial sums, y + BatchNorm-backward
+// sums (bnb_*), fp32 gradient (split / accumulate); the sums are per lane across the workgroup's tiles and
+// reduced once (one partial row per wave row group: [.. gridDim.x * 4 ..]).
+#include "conv_mfma32.h"
+
+namespace unet {
+
+constexpr int C5_W = 32, C5_HW = 34;     // tile width, halo width (pixels)
+constexpr int C5_WM = 4, C5_WN = 2, C5_NW = 8, C5_NT = 512;
+constexpr int C5_BN = 64;                // output channels per workgroup
+constexpr int C5_CMAX = 1024;            // largest BN-activation source (scale / shift table)
+constexpr int C5_NPAD = 128;             // packed weight rows are padded to this (conv.hip PACK_NPAD)
+constexpr int OM5_Y = 0, OM5_F32 = 1, OM5_BNB = 2;
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void dma16(rsrc_t r, const void* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, (int)voff, 0, 0, 0);
+}
+__device__ __forceinline__ void dma4(rsrc_t r, const void* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 4, (int)voff, 0, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]), nothing else
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void wait_vm_n(int n) {   // n is wave-uniform
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    case 8: wait_vm<8>(); break;
+    case 9: wait_vm<9>(); break;
+    case 10: wait_vm<10>(); break;
+    case 11: wait_vm<11>(); break;
+    default: wait_vm<12>(); break;
+  }
+}
+// workgroup barrier that leaves the DMA queue alone: this wave's LDS writes done, then s_barrier
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int MI, bool ACT>
+struct C5Layout {
+  static constexpr int TH = C5_WM * MI;
+  static constexpr int HP = C5_HW * (TH + 2);       // halo pixels
+  static constexpr int NS = 2 * HP;                 // 16-byte slots per chunk image
+  static constexpr int NI = (NS + 63) / 64;         // DMA instructions per image
+  static constexpr int DPW = (NI + C5_NW - 1) / C5_NW;
+  static constexpr int IMG = NS * 16;
+  static constexpr int NCOMP = ACT ? 2 : 3;
+  static constexpr int WIMG = 9 * C5_WN * 1024;     // weight fragments of one chunk
+  static constexpr int WPW = (9 * C5_WN + C5_NW - 1) / C5_NW;
+  static constexpr int OFF_COMP = 0;
+  static constexpr int OFF_RAW = OFF_COMP + NCOMP * IMG;
+  static constexpr int OFF_W = OFF_RAW + (ACT ? 2 * IMG : 0);
+  static constexpr int OFF_GATE = OFF_W + 3 * WIMG;
+  static constexpr int GATE = NI * 256;             // per-lane gate pre-activations of one tile
+  static constexpr int OFF_TAB = OFF_GATE + (ACT ? 2 * GATE : 0);
+  static constexpr int BYTES = OFF_TAB + (ACT ? 2 * C5_CMAX * 4 : 0);
+};
+
+// wave tile: MI rows x 32 px x 32 channels; SK: SK_PLAIN (every source stored as is) or SK_ACT / SK_ACT_PLAIN
+// (src0 a BN activation, optionally gated; src1 stored).  ABL (diagnostic ablations, unet_diag_conv5_ablate;
+// 0 in the product): 1 no in-loop halo DMA, 2 no in-loop weight DMA, 4 no epilogue, 8 no per-chunk barrier,
+// 16 no BN transform
+template <typename T, int MI, int OM, int SK, int ABL = 0>
+__global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d, int tiles_w, int tiles_h, int mtiles,
+                                                        int nch) {
+  using F = typename Mma32<T>::frag;
+  constexpr bool ACT = SK != SK_PLAIN;
+  using Lay = C5Layout<MI, ACT>;
+  constexpr int TH = Lay::TH, NS = Lay::NS, NI = Lay::NI, DPW = Lay::DPW, WPW = Lay::WPW;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[Lay::BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int cw0 = blockIdx.y * C5_BN + wn * 32;     // this wave's first output channel
+  const int ntl = (mtiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;   // tiles of this block
+  const int G = ntl * nch;                          // chunk steps of this block
+  auto tile_of = [&](int ti, int& n_, int& h0_, int& w0_) {
+    const int t = (int)blockIdx.x + ti * (int)gridDim.x;
+    const int tw_i = t % tiles_w;
+    const int t2 = t / tiles_w;
+    h0_ = (t2 % tiles_h) * TH;
+    w0_ = tw_i * C5_W;
+    n_ = t2 / tiles_h;
+  };
+
+  // ---- sources ----
+  const unet_src& s0 = d.src[0];
+  const unet_src& s1 = d.src[1];
+  const int C0 = s0.C;
+  const long long npix = (long long)d.N * d.H * d.W;
+  const rsrc_t rs0 = mk_rsrc(s0.data, (unsigned)(npix * C0 * 2));
+  const rsrc_t rs1 = d.nsrc > 1 ? mk_rsrc(s1.data, (unsigned)(npix * s1.C * 2)) : rs0;
+  const bool gated = ACT && s0.gate_p != nullptr;
+  const rsrc_t rsg = mk_rsrc(gated ? (const void*)s0.gate_p : s0.data, (unsigned)(npix * 4));
+  float ga = 0.f, gb = 0.f;
+  if (gated) { ga = s0.gate_ab[0]; gb = s0.gate_ab[1]; }
+  const float lo = s0.relu ? 0.f : -INFINITY;
+
+  // ---- weights: A fragment (32 output channels x 16 k) of the 16x16x32 fragment-major packing ----
+  const int nch32 = (nch + 1) >> 1;
+  const unsigned jstride = (unsigned)nch32 * 9u * 1024u;
+  const unsigned ntiles16 = (unsigned)((d.Cout + C5_NPAD - 1) / C5_NPAD * (C5_NPAD / 16));
+  const rsrc_t rw = mk_rsrc(d.weight, ntiles16 * jstride);
+  const unsigned lanew = (unsigned)((lane >> 4) & 1) * jstride + (unsigned)(16 * (lane >> 5) + (lane & 15)) * 16u;
+
+  // ---- this lane's halo DMA slots: instruction i = wave + k*NW covers slots 64 i .. 64 i + 63 ----
+  int hbit[DPW];        // logical channel half of the slot (swizzled image)
+  bool sok[DPW];        // slot inside the image
+#pragma unroll
+  for (int k = 0; k < DPW; ++k) {
+    const int i = wave + k * C5_NW, s = i * 64 + lane;
+    const int hp = s >> 1;
+    sok[k] = i < NI && s < NS;
+    hbit[k] = (s & 1) ^ ((hp >> 3) & 1);
+  }
+
+  int pxe[DPW], pxo[DPW];   // pixel index of each slot (-1: padding), for the tiles of even / odd index
+  auto geo = [&](int ti, int (&p)[DPW]) {
+    int n, h0, w0;
+    tile_of(ti, n, h0, w0);
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) {
+      const int s = (wave + k * C5_NW) * 64 + lane;
+      const int hp = s >> 1;
+      const int y = h0 - 1 + hp / C5_HW, x = w0 - 1 + hp % C5_HW;
+      p[k] = (sok[k] && y >= 0 && y < d.H && x >= 0 && x < d.W) ? (n * d.H + y) * d.W + x : -1;
+    }
+  };
+
+  // B-fragment byte offsets in a compute image: row r = wm*MI + rr (rr < MI+2), tap column dx
+  unsigned xoff[3][MI + 2];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int rr = 0; rr < MI + 2; ++rr) {
+      const int hp = (wm * MI + rr) * C5_HW + (lane & 31) + dx;
+      xoff[dx][rr] = (unsigned)(2 * hp + ((lane >> 5) ^ ((hp >> 3) & 1))) * 16u;
+    }
+
+  auto comp_buf = [&](int g) -> unsigned char* { return lds + Lay::OFF_COMP + (g % Lay::NCOMP) * Lay::IMG; };
+  auto raw_buf = [&](int g) -> unsigned char* { return lds + Lay::OFF_RAW + (g & 1) * Lay::IMG; };
+  auto w_buf = [&](int g) -> unsigned char* { return lds + Lay::OFF_W + (g % 3) * Lay::WIMG; };
+  auto gate_buf = [&](int ti) -> unsigned char* { return lds + Lay::OFF_GATE + (ti & 1) * Lay::GATE; };
+
+  // DMA of chunk step g (tile g / nch, channels 16 (g % nch) ..): halo slots, weight fragments, and at the
+  // tile's first chunk the gate pre-activations of this lane's slots; returns the instructions issued
+  auto issue = [&](int g) -> int {
+    const int ti = g / nch, c = g - ti * nch;
+    if (c == 0) {
+      if (ti & 1) geo(ti, pxo);
+      else geo(ti, pxe);
+    }
+    int p[DPW];
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) p[k] = (ti & 1) ? pxo[k] : pxe[k];
+    const int cn0 = c * 16;
+    const int si = (d.nsrc > 1 && cn0 >= C0) ? 1 : 0;
+    const int cl = cn0 - (si ? C0 : 0);
+    const int Cs = si ? s1.C : C0;
+    const rsrc_t rs = si ? rs1 : rs0;
+    unsigned char* dst = ACT ? raw_buf(g) : comp_buf(g);
+    int cnt = 0;
+    const bool abl_h = (ABL & 1) && g >= 2, abl_w = (ABL & 2) && g >= 2;
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) {
+      const int i = wave + k * C5_NW;
+      if (i < NI && !abl_h) {
+        const int ch = cl + 8 * hbit[k];
+        const unsigned vo = (p[k] >= 0 && ch < Cs) ? ((unsigned)p[k] * (unsigned)Cs + (unsigned)ch) * 2u : OOB;
+        if (sok[k]) dma16(rs, dst + i * 1024, vo);
+        ++cnt;
+      }
+    }
+    unsigned char* wd = w_buf(g);
+#pragma unroll
+    for (int k = 0; k < WPW; ++k) {
+      const int j = wave + k * C5_NW;
+      if (j < 9 * C5_WN && !abl_w) {
+        const int tap = j >> 1, wj = j & 1;
+        const unsigned nt0 = (unsigned)((blockIdx.y * C5_BN + wj * 32) / 16);
+        dma16(rw, wd + j * 1024,
+              lanew + nt0 * jstride + (unsigned)((c >> 1) * 9 + tap) * 1024u + (unsigned)(c & 1) * 512u);
+        ++cnt;
+      }
+    }
+    if (gated && c == 0) {
+#pragma unroll
+      for (int k = 0; k < DPW; ++k) {
+        const int i = wave + k * C5_NW;
+        if (i < NI) {
+          if (sok[k]) dma4(rsg, gate_buf(ti) + i * 256, p[k] >= 0 ? (unsigned)p[k] * 4u : OOB);
+          ++cnt;
+        }
+      }
+    }
+    return cnt;
+  };
+
+  // BN-activation (+gate) transform of chunk step g, raw -> compute image, this lane's own DMA slots
+  auto transform = [&](int g) {
+    const int ti = g / nch, c = g - ti * nch;
+    int p[DPW];
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) p[k] = (ti & 1) ? pxo[k] : pxe[k];
+    const int cn0 = c * 16;
+    const bool act = !(d.nsrc > 1 && cn0 >= C0);    // src0 (activation) or src1 (stored: copied)
+    const unsigned char* rb = raw_buf(g);
+    unsigned char* cb = comp_buf(g);
+    const float* tab = reinterpret_cast<const float*>(lds + Lay::OFF_TAB);
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) {
+      const int i = wave + k * C5_NW;
+      if (i < NI && sok[k]) {
+        const int s = i * 64 + lane;
+        uint4 q = *reinterpret_cast<const uint4*>(rb + s * 16);
+        if (act) {
+          const int ch = cn0 + 8 * hbit[k];
+          const bool ok = p[k] >= 0 && ch < C0;
+          const float4 a0 = *reinterpret_cast<const float4*>(tab + (ok ? ch : 0));
+          const float4 a1 = *reinterpret_cast<const float4*>(tab + (ok ? ch : 0) + 4);
+          const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_CMAX + (ok ? ch : 0));
+          const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_CMAX + (ok ? ch : 0) + 4);
+          const float sc[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          const float sf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+          float gm = ok ? 1.f : 0.f;
+          if (gated) {
+            const float pv = *reinterpret_cast<const float*>(gate_buf(ti) + i * 256 + lane * 4);
+            gm = ok ? sigmoidf_(pv * ga + gb) : 0.f;
+          }
+          float v[8];
+          unpack8_16<T>(q, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo) * gm;
+          q = pack8_16<T>(v);
+        }
+        *reinterpret_cast<uint4*>(cb + s * 16) = q;
+      }
+    }
+  };
+
+  // ---- prologue: scale/shift table, chunks 0 and 1 in flight, chunk 0 ready ----
+  if constexpr (ACT) {
+    float* tab = reinterpret_cast<float*>(lds + Lay::OFF_TAB);
+    for (int c = tid; c < C0; c += C5_NT) { tab[c] = s0.scale[c]; tab[C5_CMAX + c] = s0.shift[c]; }
+    if (tid < 8) { tab[C0 + tid] = 0.f; tab[C5_CMAX + C0 + tid] = 0.f; }
+  }
+  issue(0);
+  if (G > 1) issue(1);
+  wait_vm<0>();
+  if constexpr (ACT) {
+    lds_barrier();      // the scale/shift table
+    transform(0);
+  }
+  lds_barrier();
+
+  // BatchNorm sums of this lane's pixel column over the block's tiles (see conv4.hip)
+  constexpr bool SUMS = OM == OM5_Y || OM == OM5_BNB;
+  float sA[16], sB[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { sA[r] = 0.f; sB[r] = 0.f; }
+  f32x16 acc[MI];
+
+  int g = 0;
+  for (int ti = 0; ti < ntl; ++ti) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c, ++g) {
+      const int nd = (g + 2 < G) ? issue(g + 2) : 0;
+      const unsigned char* xb = comp_buf(g);
+      const unsigned char* wb = w_buf(g) + wn * 1024 + lane * 16;
+      F xr[MI + 2];
+#pragma unroll
+      for (int st = 0; st < 9; ++st) {
+        const int dx = st / 3, dy = st % 3, t = dy * 3 + dx;
+        if (dy == 0) {
+#pragma unroll
+          for (int rr = 0; rr < MI + 2; ++rr) xr[rr] = *reinterpret_cast<const F*>(xb + xoff[dx][rr]);
+        }
+        const F a = *reinterpret_cast<const F*>(wb + t * 2048);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) acc[i] = Mma32<T>::mma(a, xr[i + dy], acc[i]);
+        if (st == 4) {
+          wait_vm_n(nd);                 // this wave's DMAs of step g+1 (issued one step ago) have landed
+          if constexpr (ACT && !(ABL & 16)) {
+            if (g + 1 < G) transform(g + 1);
+          }
+        }
+      }
+      if constexpr (!(ABL & 8)) lds_barrier();
+    }
+
+    // ---------------- epilogue of tile ti ----------------
+    if constexpr (ABL & 4) {
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) sum += acc[i][0] + acc[i][7] + acc[i][15];
+      if (sum == 12345.f) ((float*)d.out)[tid] = sum;
+      continue;
+    }
+    int n, h0, w0;
+    tile_of(ti, n, h0, w0);
+    const int pxl = lane & 31, hh = lane >> 5;
+    const int ow = w0 + pxl;
+    const bool colok = ow < d.W;
+    const int oh0 = h0 + wm * MI;
+    int rows = d.H - oh0;
+    rows = rows < 0 ? 0 : (rows > MI ? MI : rows);
+    const unsigned pix0 = ((unsigned)n * d.H + oh0) * (unsigned)d.W + ow;
+    if constexpr (OM == OM5_Y) {
+      T* y = (T*)d.out;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const bool ok = colok && i < rows;
+        const unsigned pix = pix0 + (unsigned)i * d.W;
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int co = cw0 + 8 * gq + 4 * hh;
+          if (ok && co < d.Cout) {
+            uint2 pk;
+            pk.x = pack2_16<T>(acc[i][4 * gq], acc[i][4 * gq + 1]);
+            pk.y = pack2_16<T>(acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
+            *reinterpret_cast<uint2*>(y + (size_t)pix * d.Cout + co) = pk;
+          }
+        }
+      }
+      if (d.stats) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const float x = (colok && i < rows) ? acc[i][r] : 0.f;
+            sA[r] += x;
+            sB[r] = __builtin_fmaf(x, x, sB[r]);
+          }
+      }
+    } else if constexpr (OM == OM5_BNB) {
+      T* y = (T*)d.out;
+      const T* y1 = (const T*)d.bnb_y;
+      uint2 yv[MI][4];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int co = cw0 + 8 * gq + 4 * hh;
+          yv[i][gq] = make_uint2(0u, 0u);
+          if (colok && i < rows && co < d.Cout)
+            yv[i][gq] = *reinterpret_cast<const uint2*>(y1 + (size_t)(pix0 + (unsigned)i * d.W) * d.Cout + co);
+        }
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int co = cw0 + 8 * gq + 4 * hh;
+        const bool cok = co < d.Cout;
+        float sc4[4] = {0.f, 0.f, 0.f, 0.f}, sf4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (cok && d.bnb_relu) {
+          const float4 a4 = *reinterpret_cast<const float4*>(d.bnb_scale + co);
+          const float4 b4 = *reinterpret_cast<const float4*>(d.bnb_shift + co);
+          sc4[0] = a4.x; sc4[1] = a4.y; sc4[2] = a4.z; sc4[3] = a4.w;
+          sf4[0] = b4.x; sf4[1] = b4.y; sf4[2] = b4.z; sf4[3] = b4.w;
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const unsigned pix = pix0 + (unsigned)i * d.W;
+          if (colok && i < rows && cok) {
+            uint2 pk;
+            pk.x = pack2_16<T>(acc[i][4 * gq], acc[i][4 * gq + 1]);
+            pk.y = pack2_16<T>(acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
+            *reinterpret_cast<uint2*>(y + (size_t)pix * d.Cout + co) = pk;
+            float gv[4], yy[4];
+            unpack4_16<T>(pk, gv);
+            unpack4_16<T>(yv[i][gq], yy);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float gg = (d.bnb_relu && !(yy[r] * sc4[r] + sf4[r] > 0.f)) ? 0.f : gv[r];
+              sA[4 * gq + r] += gg;
+              sB[4 * gq + r] = __builtin_fmaf(gg, yy[r], sB[4 * gq + r]);
+            }
+          }
+        }
+      }
+    } else {  // OM5_F32
+      float* o1 = (float*)d.out;
+      float* o2 = (float*)d.out2;
+      const int c2 = d.Cout - d.split;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        if (!(colok && i < rows)) continue;
+        const unsigned pix = pix0 + (unsigned)i * d.W;
+        float4* pp[4];
+        float4 old[4];
+        bool acc_in[4];
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int co = cw0 + 8 * gq + 4 * hh;
+          if (co < d.split) {
+            pp[gq] = reinterpret_cast<float4*>(o1 + (size_t)pix * d.split + co);
+            acc_in[gq] = d.accum;
+          } else {
+            pp[gq] = reinterpret_cast<float4*>(o2 + (size_t)pix * c2 + (co - d.split));
+            acc_in[gq] = d.accum2;
+          }
+          old[gq] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (co < d.Cout && acc_in[gq]) old[gq] = *pp[gq];
+        }
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int co = cw0 + 8 * gq + 4 * hh;
+          if (co < d.Cout) {
+            float4 w = make_float4(acc[i][4 * gq], acc[i][4 * gq + 1], acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
+            if (acc_in[gq]) { w.x += old[gq].x; w.y += old[gq].y; w.z += old[gq].z; w.w += old[gq].w; }
+            *pp[gq] = w;
+          }
+        }
+      }
+    }
+  }
+
+  // ---- the workgroup's BatchNorm sums: one partial row per wave row group ----
+  if constexpr (SUMS) {
+    const int hh = lane >> 5;
+    const int srow = blockIdx.x * C5_WM + wm, srows = gridDim.x * C5_WM;
+    if constexpr (OM == OM5_Y) {
+      if (d.stats) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float a = half32_sum(sA[r]), b = half32_sum(sB[r]);
+          const int co = cw0 + 8 * (r >> 2) + 4 * hh + (r & 3);
+          if ((lane & 31) == 0 && co < d.Cout) {
+            d.stats[(size_t)co * srows + srow] = a;
+            d.stats[((size_t)d.Cout + co) * srows + srow] = b;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int co = cw0 + 8 * gq + 4 * hh;
+        float a[4], b[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = half32_sum(sA[4 * gq + r]);
+          b[r] = half32_sum(sB[4 * gq + r]);
+        }
+        if ((lane & 31) == 0 && co < d.Cout) {
+          const float4 m4 = *reinterpret_cast<const float4*>(d.bnb_mean + co);
+          const float4 i4 = *reinterpret_cast<const float4*>(d.bnb_invstd + co);
+          const float mu[4] = {m4.x, m4.y, m4.z, m4.w}, is[4] = {i4.x, i4.y, i4.z, i4.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) b[r] = is[r] * (b[r] - mu[r] * a[r]);
+          *reinterpret_cast<float4*>(d.bnb_stats + (size_t)srow * d.Cout + co) = make_float4(a[0], a[1], a[2], a[3]);
+          *reinterpret_cast<float4*>(d.bnb_stats + ((size_t)srows + srow) * d.Cout + co) =
+              make_float4(b[0], b[1], b[2], b[3]);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+constexpr int C5_MI = 4;
+
+// UNET_CONV5=0 routes the eligible convs back to conv3 (A/B switch; read per call so tests can flip it)
+static bool conv5_enabled() {
+  const char* e = getenv("UNET_CONV5");
+  return !(e && atoi(e) == 0);
+}
+
+static long long conv5_mtiles(const unet_conv_desc* d) {
+  return (long long)d->N * cdiv(d->W, C5_W) * cdiv(d->H, C5_WM * C5_MI);
+}
+
+static int conv5_gx(const unet_conv_desc* d) {
+  const long long mt = conv5_mtiles(d);
+  const int gy = cdiv(d->Cout, C5_BN);
+  long long gx = cdiv(256, gy);                     // one 8-wave workgroup per CU (LDS), persistent
+  if (gx > mt) gx = mt;
+  if (gx < 1) gx = 1;
+  return (int)gx;
+}
+
+// 16-bit 3x3; stored or BN-activation sources (src0 may be gated, src1 stored; the network's pooled and
+// upsampled maps are materialised), Cin > 16 (two chunks in flight), a BN activation of <= 1024 channels,
+// y / y + BN-backward sums / fp32 epilogues, enough 16 x 32 tiles to fill the chip
+bool conv5_eligible(const unet_conv_desc* d) {
+  if (!conv5_enabled()) return false;
+  if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 3) return false;
+  if (d->out_mode != UNET_OUT_Y && d->out_mode != UNET_OUT_F32) return false;
+  if (d->Cout % 4 || (d->out_mode == UNET_OUT_F32 && d->split % 4)) return false;
+  if (d->Cin <= 16) return false;
+  if (d->nsrc > 1 && (d->src[0].C % 16 || d->src[1].kind != UNET_SRC_PLAIN || d->src[1].gate_p)) return false;
+  const unet_src& s0 = d->src[0];
+  if (s0.kind != UNET_SRC_PLAIN && s0.kind != UNET_SRC_ACT) return false;
+  if (s0.kind == UNET_SRC_PLAIN && s0.gate_p) return false;
+  if (s0.kind == UNET_SRC_ACT && s0.C > C5_CMAX) return false;
+  for (int i = 0; i < d->nsrc; ++i) {
+    const unet_src& s = d->src[i];
+    if (s.C % 8) return false;
+    if ((double)d->N * s.H * s.W * s.C * 2 >= (double)OOB) return false;
+    if (s.H != d->H || s.W != d->W) return false;
+  }
+  if ((double)d->N * d->H * d->W * 4 >= (double)OOB) return false;
+  const long long work = conv5_mtiles(d) * cdiv(d->Cout, C5_BN);
+  return work >= 256;
+}
+
+int conv5_stats_rows(const unet_conv_desc* d) { return conv5_gx(d) * C5_WM; }
+
+int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
+  snprintf(buf, len, "conv5_kernel<%s,%d>", d->dtype == UNET_F16 ? "fp16" : "bf16", C5_MI);
+  return 0;
+}
+
+template <typename T, int OM, int SK, int ABL = 0>
+static int launch5(const unet_conv_desc* d, hipStream_t st) {
+  constexpr int TH = C5_WM * C5_MI;
+  const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH);
+  const int mt = d->N * tw * th;
+  const int gy = cdiv(d->Cout, C5_BN);
+  const int gx = conv5_gx(d);
+  hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, ABL>), dim3(gx, gy), dim3(C5_NT), 0, st, *d, tw, th, mt,
+                     cdiv(d->Cin, 16));
+  return check_launch("conv5");
+}
+
+template <typename T>
+static int dispatch5(const unet_conv_desc* d, hipStream_t st) {
+  const bool act = d->src[0].kind == UNET_SRC_ACT;
+  if (d->out_mode == UNET_OUT_F32)
+    return act ? launch5<T, OM5_F32, SK_ACT>(d, st) : launch5<T, OM5_F32, SK_PLAIN>(d, st);
+  if (d->bnb_stats)
+    return act ? launch5<T, OM5_BNB, SK_ACT>(d, st) : launch5<T, OM5_BNB, SK_PLAIN>(d, st);
+  return act ? launch5<T, OM5_Y, SK_ACT>(d, st) : launch5<T, OM5_Y, SK_PLAIN>(d, st);
+}
+
+int conv5_run(const unet_conv_desc* d, hipStream_t st) {
+  return d->dtype == UNET_F16 ? dispatch5<f16>(d, st) : dispatch5<bf16>(d, st);
+}
+
+template <int SK>
+static int abl5(const unet_conv_desc* d, int abl, hipStream_t st) {
+  switch (abl) {
+    case 0: return launch5<bf16, OM5_Y, SK, 0>(d, st);
+    case 1: return launch5<bf16, OM5_Y, SK, 1>(d, st);
+    case 2: return launch5<bf16, OM5_Y, SK, 2>(d, st);
+    case 3: return launch5<bf16, OM5_Y, SK, 3>(d, st);
+    case 4: return launch5<bf16, OM5_Y, SK, 4>(d, st);
+    case 8: return launch5<bf16, OM5_Y, SK, 8>(d, st);
+    case 7: return launch5<bf16, OM5_Y, SK, 7>(d, st);
+    case 15: return launch5<bf16, OM5_Y, SK, 15>(d, st);
+    case 16: return launch5<bf16, OM5_Y, SK, 16>(d, st);
+    case 31: return launch5<bf16, OM5_Y, SK, 31>(d, st);
+  }
+  return UNET_ERR_ARG;
+}
+
+}  // namespace unet
+
+// diagnostic (not part of the C ABI header): conv5 ablations of the bf16 y-mode kernel (ABL bits above) on a
+// one-source plain or BN-activation descriptor; tools/conv4_ablate.py --conv5
+extern "C" int unet_diag_conv5_ablate(const unet_conv_desc* d, int abl, void* stream) {
+  using namespace unet;
+  if (!conv5_eligible(d) || d->nsrc != 1 || d->out_mode != UNET_OUT_Y || d->dtype != UNET_BF16) return UNET_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return d->src[0].kind == UNET_SRC_PLAIN ? abl5<SK_PLAIN>(d, abl, st) : abl5<SK_ACT>(d, abl, st);
+}

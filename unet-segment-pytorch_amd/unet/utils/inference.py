@@ -84,10 +84,12 @@ class GraphedPredictor:
         with torch.no_grad(), torch.cuda.graph(self.graph):
             self.out = self.model(self.x)
 
-    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, copy: bool = True) -> torch.Tensor:
+        """Logits of x.  copy=False returns the graph's static output buffer itself, which the next call
+        overwrites (no extra 8-byte-per-logit copy); the default returns an independent tensor."""
         self.x.copy_(x, non_blocking=True)
         self.graph.replay()
-        return self.out
+        return self.out.clone() if copy else self.out
 
 
 def predict_masks(model: torch.nn.Module, images: torch.Tensor, img_size: int = 256, threshold: float = 0.5,
