@@ -41,19 +41,44 @@ constexpr int C5_CMAX = 1024;            // largest BN-activation source (scale 
 constexpr int C5_NPAD = 128;             // packed weight rows are padded to this (conv.hip PACK_NPAD)
 constexpr int OM5_Y = 0, OM5_F32 = 1, OM5_BNB = 2;
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) const void* lds_ptr_t;
+typedef __attribute__((ext_vector_type(4))) unsigned rsrc4_t;   // buffer resource as an SGPR quad
 
-__device__ __forceinline__ void dma16(rsrc_t r, const void* lds, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 16, (int)voff, 0, 0, 0);
-}
-__device__ __forceinline__ void dma4(rsrc_t r, const void* lds, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)lds, 4, (int)voff, 0, 0, 0);
+// raw buffer resource (range = bytes, OOB loads return 0) for the inline-asm DMAs below
+__device__ __forceinline__ rsrc4_t mk_rsrc4(const void* p, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  rsrc4_t r;
+  r.x = __builtin_amdgcn_readfirstlane((unsigned)a);
+  r.y = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32) & 0xffffu);
+  r.z = __builtin_amdgcn_readfirstlane(bytes);
+  r.w = 0x00020000u;
+  return r;
 }
 
-// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]), nothing else
+// LDS DMA (buffer_load ... lds: M0 = wave-uniform LDS base, lane l lands at base + l * size).  Issued as
+// inline asm on purpose: the compiler's waitcnt pass treats every LDS read that may alias an outstanding
+// LDS-DMA write as dependent on it and puts s_waitcnt vmcnt(0) in front of it — which drains the two-chunk
+// prefetch on every chunk.  The kernel orders its DMAs itself (wait_vm per chunk + lds_barrier); the asm's
+// memory clobber keeps the compiler from moving LDS accesses across the issue.  The s_nop 4 supplies the
+// wait states the compiler's hazard recognizer inserts for the builtin but cannot see inside an asm
+// statement: 5 between a VALU write of an SGPR (v_readlane of a resource spilled to VGPR lanes,
+// v_readfirstlane) and a VMEM instruction reading it, 1 between an SALU write of M0 and an LDS DMA.
+__device__ __forceinline__ unsigned lds_addr(const void* lds) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(lds_ptr_t)lds);
+}
+__device__ __forceinline__ void dma16(rsrc4_t r, const void* lds, unsigned voff) {
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "{m0}"(lds_addr(lds))
+               : "memory");
+}
+__device__ __forceinline__ void dma4(rsrc4_t r, const void* lds, unsigned voff) {
+  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "{m0}"(lds_addr(lds))
+               : "memory");
+}
+
+// s_waitcnt vmcnt(N), nothing else; asm with a memory clobber so no LDS read is hoisted above it
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void wait_vm_n(int n) {   // n is wave-uniform
   switch (n) {
@@ -132,10 +157,10 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   const unet_src& s1 = d.src[1];
   const int C0 = s0.C;
   const long long npix = (long long)d.N * d.H * d.W;
-  const rsrc_t rs0 = mk_rsrc(s0.data, (unsigned)(npix * C0 * 2));
-  const rsrc_t rs1 = d.nsrc > 1 ? mk_rsrc(s1.data, (unsigned)(npix * s1.C * 2)) : rs0;
+  const rsrc4_t rs0 = mk_rsrc4(s0.data, (unsigned)(npix * C0 * 2));
+  const rsrc4_t rs1 = d.nsrc > 1 ? mk_rsrc4(s1.data, (unsigned)(npix * s1.C * 2)) : rs0;
   const bool gated = ACT && s0.gate_p != nullptr;
-  const rsrc_t rsg = mk_rsrc(gated ? (const void*)s0.gate_p : s0.data, (unsigned)(npix * 4));
+  const rsrc4_t rsg = mk_rsrc4(gated ? (const void*)s0.gate_p : s0.data, (unsigned)(npix * 4));
   float ga = 0.f, gb = 0.f;
   if (gated) { ga = s0.gate_ab[0]; gb = s0.gate_ab[1]; }
   const float lo = s0.relu ? 0.f : -INFINITY;
@@ -144,30 +169,33 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   const int nch32 = (nch + 1) >> 1;
   const unsigned jstride = (unsigned)nch32 * 9u * 1024u;
   const unsigned ntiles16 = (unsigned)((d.Cout + C5_NPAD - 1) / C5_NPAD * (C5_NPAD / 16));
-  const rsrc_t rw = mk_rsrc(d.weight, ntiles16 * jstride);
+  const rsrc4_t rw = mk_rsrc4(d.weight, ntiles16 * jstride);
   const unsigned lanew = (unsigned)((lane >> 4) & 1) * jstride + (unsigned)(16 * (lane >> 5) + (lane & 15)) * 16u;
 
   // ---- this lane's halo DMA slots: instruction i = wave + k*NW covers slots 64 i .. 64 i + 63 ----
   int hbit[DPW];        // logical channel half of the slot (swizzled image)
   bool sok[DPW];        // slot inside the image
+  int soy[DPW], sox[DPW];   // the slot's pixel offset from the tile origin (halo: -1 .. TH, -1 .. 32)
 #pragma unroll
   for (int k = 0; k < DPW; ++k) {
     const int i = wave + k * C5_NW, s = i * 64 + lane;
     const int hp = s >> 1;
     sok[k] = i < NI && s < NS;
     hbit[k] = (s & 1) ^ ((hp >> 3) & 1);
+    soy[k] = hp / C5_HW - 1;
+    sox[k] = hp % C5_HW - 1;
   }
 
-  int pxe[DPW], pxo[DPW];   // pixel index of each slot (-1: padding), for the tiles of even / odd index
+  // pixel index of each of this lane's slots for tile ti (-1: zero padding / past the image).  Recomputed
+  // per chunk (a few VALU per slot) rather than kept per tile: a per-tile array selected by tile parity was
+  // put in scratch, and scratch loads share vmcnt with the DMAs
   auto geo = [&](int ti, int (&p)[DPW]) {
     int n, h0, w0;
     tile_of(ti, n, h0, w0);
 #pragma unroll
     for (int k = 0; k < DPW; ++k) {
-      const int s = (wave + k * C5_NW) * 64 + lane;
-      const int hp = s >> 1;
-      const int y = h0 - 1 + hp / C5_HW, x = w0 - 1 + hp % C5_HW;
-      p[k] = (sok[k] && y >= 0 && y < d.H && x >= 0 && x < d.W) ? (n * d.H + y) * d.W + x : -1;
+      const int y = h0 + soy[k], x = w0 + sox[k];
+      p[k] = (sok[k] && (unsigned)y < (unsigned)d.H && (unsigned)x < (unsigned)d.W) ? (n * d.H + y) * d.W + x : -1;
     }
   };
 
@@ -190,18 +218,13 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   // tile's first chunk the gate pre-activations of this lane's slots; returns the instructions issued
   auto issue = [&](int g) -> int {
     const int ti = g / nch, c = g - ti * nch;
-    if (c == 0) {
-      if (ti & 1) geo(ti, pxo);
-      else geo(ti, pxe);
-    }
     int p[DPW];
-#pragma unroll
-    for (int k = 0; k < DPW; ++k) p[k] = (ti & 1) ? pxo[k] : pxe[k];
+    geo(ti, p);
     const int cn0 = c * 16;
     const int si = (d.nsrc > 1 && cn0 >= C0) ? 1 : 0;
     const int cl = cn0 - (si ? C0 : 0);
     const int Cs = si ? s1.C : C0;
-    const rsrc_t rs = si ? rs1 : rs0;
+    const rsrc4_t rs = si ? rs1 : rs0;
     unsigned char* dst = ACT ? raw_buf(g) : comp_buf(g);
     int cnt = 0;
     const bool abl_h = (ABL & 1) && g >= 2, abl_w = (ABL & 2) && g >= 2;
@@ -244,8 +267,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   auto transform = [&](int g) {
     const int ti = g / nch, c = g - ti * nch;
     int p[DPW];
-#pragma unroll
-    for (int k = 0; k < DPW; ++k) p[k] = (ti & 1) ? pxo[k] : pxe[k];
+    geo(ti, p);
     const int cn0 = c * 16;
     const bool act = !(d.nsrc > 1 && cn0 >= C0);    // src0 (activation) or src1 (stored: copied)
     const unsigned char* rb = raw_buf(g);
@@ -359,15 +381,22 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       for (int i = 0; i < MI; ++i) {
         const bool ok = colok && i < rows;
         const unsigned pix = pix0 + (unsigned)i * d.W;
+        // lane l < 32 holds channels 8gq+0..3 of pixel l, lane l+32 channels 8gq+4..7 of the same pixel:
+        // v_permlane32_swap of the packed groups (gq, gq+1) leaves lanes 0-31 with channels 8gq..8gq+7 and
+        // lanes 32-63 with 8gq+8..8gq+15 — one 16-byte store per pair instead of two 8-byte ones
+        unsigned px_[4], py_[4];
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          const int co = cw0 + 8 * gq + 4 * hh;
-          if (ok && co < d.Cout) {
-            uint2 pk;
-            pk.x = pack2_16<T>(acc[i][4 * gq], acc[i][4 * gq + 1]);
-            pk.y = pack2_16<T>(acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
-            *reinterpret_cast<uint2*>(y + (size_t)pix * d.Cout + co) = pk;
-          }
+          px_[gq] = pack2_16<T>(acc[i][4 * gq], acc[i][4 * gq + 1]);
+          py_[gq] = pack2_16<T>(acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
+        }
+#pragma unroll
+        for (int kp = 0; kp < 4; kp += 2) {
+          const auto sx = __builtin_amdgcn_permlane32_swap(px_[kp], px_[kp + 1], false, false);
+          const auto sy = __builtin_amdgcn_permlane32_swap(py_[kp], py_[kp + 1], false, false);
+          const int co = cw0 + 8 * kp + 8 * hh;
+          if (ok && co < d.Cout)
+            *reinterpret_cast<uint4*>(y + (size_t)pix * d.Cout + co) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
         }
       }
       if (d.stats) {
@@ -507,10 +536,11 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
 // ------------------------------------------------------------------------------------------------
 constexpr int C5_MI = 4;
 
-// UNET_CONV5=0 routes the eligible convs back to conv3 (A/B switch; read per call so tests can flip it)
-static bool conv5_enabled() {
+// UNET_CONV5: unset = the measured default (below), 0 = never (conv3 everywhere), 1 = every eligible conv
+// (tests, ablations); read per call so tests can flip it
+static int conv5_mode() {
   const char* e = getenv("UNET_CONV5");
-  return !(e && atoi(e) == 0);
+  return e ? (atoi(e) ? 1 : 0) : 2;
 }
 
 static long long conv5_mtiles(const unet_conv_desc* d) {
@@ -530,10 +560,15 @@ static int conv5_gx(const unet_conv_desc* d) {
 // upsampled maps are materialised), Cin > 16 (two chunks in flight), a BN activation of <= 1024 channels,
 // y / y + BN-backward sums / fp32 epilogues, enough 16 x 32 tiles to fill the chip
 bool conv5_eligible(const unet_conv_desc* d) {
-  if (!conv5_enabled()) return false;
+  const int mode = conv5_mode();
+  if (mode == 0) return false;
+  // default: the 16-bit y outputs of <= 64 channels (the 512^2 / 256^2 encoder-decoder ends), where
+  // conv5 measured 10-25 % faster than conv3 (profiles/r03_layerprof_*.txt); conv3 keeps the wider
+  // layers and the fp32 dgrads, where its 16x16x32 tiles over the full Cout measured faster
+  if (mode == 2 && (d->Cout > C5_BN || d->out_mode != UNET_OUT_Y)) return false;
   if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 3) return false;
   if (d->out_mode != UNET_OUT_Y && d->out_mode != UNET_OUT_F32) return false;
-  if (d->Cout % 4 || (d->out_mode == UNET_OUT_F32 && d->split % 4)) return false;
+  if (d->Cout % 8 || (d->out_mode == UNET_OUT_F32 && d->split % 4)) return false;   // 16-byte y stores
   if (d->Cin <= 16) return false;
   if (d->nsrc > 1 && (d->src[0].C % 16 || d->src[1].kind != UNET_SRC_PLAIN || d->src[1].gate_p)) return false;
   const unet_src& s0 = d->src[0];
