@@ -51,3 +51,32 @@ for name, fn in (("forward", fwd), ("fwd+bwd", fwd_bwd), ("step", step)):
         tot.append(t2 - t0)
     opt.zero_grad(set_to_none=True)
     print(f"{name:8s}: host enqueue {min(cpu) * 1e3:7.3f} ms, enqueue+drain {min(tot) * 1e3:7.3f} ms", flush=True)
+
+# the same step captured once and replayed (unet.utils.graphed.GraphedTrainStep; capturable fused AdamW)
+from unet.utils.graphed import GraphedTrainStep
+torch.manual_seed(0)
+m2 = AttentionUNet(1, 2).to(dev).train()
+m2.hip_precision = "bf16"
+opt2 = torch.optim.AdamW(m2.parameters(), lr=5e-5, weight_decay=1e-4, fused=True, capturable=True)
+gs = GraphedTrainStep(m2, crit, opt2, x.shape, t.shape)
+for _ in range(3):
+    gs(x, t)
+cpu, tot = [], []
+for _ in range(10):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gs(x, t)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    cpu.append(t1 - t0)
+    tot.append(t2 - t0)
+print(f"{'graphed':8s}: host enqueue {min(cpu) * 1e3:7.3f} ms, enqueue+drain {min(tot) * 1e3:7.3f} ms", flush=True)
+for name, fn in (("eager step", step), ("graphed step", lambda: gs(x, t))):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(30):
+        fn()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 30
+    print(f"{name:12s}: {dt * 1e3:7.3f} ms/step back to back = {4 / dt:7.1f} img/s", flush=True)

@@ -66,36 +66,18 @@ __device__ __forceinline__ rsrc4_t mk_rsrc4(const void* p, unsigned bytes) {
 __device__ __forceinline__ unsigned lds_addr(const void* lds) {
   return __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(lds_ptr_t)lds);
 }
-__device__ __forceinline__ void dma16(rsrc4_t r, const void* lds, unsigned voff) {
-  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "{m0}"(lds_addr(lds))
-               : "memory");
+// m0: the wave-uniform LDS byte address (an SGPR value)
+__device__ __forceinline__ void dma16(rsrc4_t r, unsigned m0, unsigned voff) {
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "{m0}"(m0) : "memory");
 }
-__device__ __forceinline__ void dma4(rsrc4_t r, const void* lds, unsigned voff) {
-  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "{m0}"(lds_addr(lds))
-               : "memory");
+__device__ __forceinline__ void dma4(rsrc4_t r, unsigned m0, unsigned voff) {
+  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "{m0}"(m0) : "memory");
 }
 
 // s_waitcnt vmcnt(N), nothing else; asm with a memory clobber so no LDS read is hoisted above it
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void wait_vm_n(int n) {   // n is wave-uniform
-  switch (n) {
-    case 0: wait_vm<0>(); break;
-    case 1: wait_vm<1>(); break;
-    case 2: wait_vm<2>(); break;
-    case 3: wait_vm<3>(); break;
-    case 4: wait_vm<4>(); break;
-    case 5: wait_vm<5>(); break;
-    case 6: wait_vm<6>(); break;
-    case 7: wait_vm<7>(); break;
-    case 8: wait_vm<8>(); break;
-    case 9: wait_vm<9>(); break;
-    case 10: wait_vm<10>(); break;
-    case 11: wait_vm<11>(); break;
-    default: wait_vm<12>(); break;
-  }
 }
 // workgroup barrier that leaves the DMA queue alone: this wave's LDS writes done, then s_barrier
 __device__ __forceinline__ void lds_barrier() {
@@ -111,7 +93,7 @@ struct C5Layout {
   static constexpr int NS = 2 * HP;                 // 16-byte slots per chunk image
   static constexpr int NI = (NS + 63) / 64;         // DMA instructions per image
   static constexpr int DPW = (NI + C5_NW - 1) / C5_NW;
-  static constexpr int IMG = NS * 16;
+  static constexpr int IMG = NI * 1024;             // padded: the last instruction's tail lanes land inside
   static constexpr int NCOMP = ACT ? 2 : 3;
   static constexpr int WIMG = 9 * C5_WN * 1024;     // weight fragments of one chunk
   static constexpr int WPW = (9 * C5_WN + C5_NW - 1) / C5_NW;
@@ -121,7 +103,8 @@ struct C5Layout {
   static constexpr int OFF_GATE = OFF_W + 3 * WIMG;
   static constexpr int GATE = NI * 256;             // per-lane gate pre-activations of one tile
   static constexpr int OFF_TAB = OFF_GATE + (ACT ? 2 * GATE : 0);
-  static constexpr int BYTES = OFF_TAB + (ACT ? 2 * C5_CMAX * 4 : 0);
+  static constexpr int OFF_JUNK = OFF_TAB + (ACT ? 2 * C5_CMAX * 4 : 0);   // target of the filler DMAs
+  static constexpr int BYTES = OFF_JUNK + 1024;
 };
 
 // wave tile: MI rows x 32 px x 32 channels; SK: SK_PLAIN (every source stored as is) or SK_ACT / SK_ACT_PLAIN
@@ -173,31 +156,24 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   const unsigned lanew = (unsigned)((lane >> 4) & 1) * jstride + (unsigned)(16 * (lane >> 5) + (lane & 15)) * 16u;
 
   // ---- this lane's halo DMA slots: instruction i = wave + k*NW covers slots 64 i .. 64 i + 63 ----
+  // Every wave issues the same, compile-time number of DMA instructions per chunk (ND; + DPW gate loads at
+  // a gated tile's first chunk), with no per-lane branch: instructions past the image go to a junk slot,
+  // lanes past it (the last instruction's tail, inside the 1 KB-padded image) and zero-padding pixels load
+  // out of range (zeros).  So the per-chunk wait is an immediate vmcnt and the chunk loop carries almost no
+  // scalar work — the scalar unit is shared by the CU's 8 waves, and a version with per-slot exec branches,
+  // divisions for the tile geometry and a switch over the wait count issued ~360 SALU per 36 MFMAs per
+  // wave (SQ_INSTS_SALU), which paced the loop
   int hbit[DPW];        // logical channel half of the slot (swizzled image)
-  bool sok[DPW];        // slot inside the image
   int soy[DPW], sox[DPW];   // the slot's pixel offset from the tile origin (halo: -1 .. TH, -1 .. 32)
 #pragma unroll
   for (int k = 0; k < DPW; ++k) {
     const int i = wave + k * C5_NW, s = i * 64 + lane;
     const int hp = s >> 1;
-    sok[k] = i < NI && s < NS;
     hbit[k] = (s & 1) ^ ((hp >> 3) & 1);
-    soy[k] = hp / C5_HW - 1;
+    soy[k] = s < NS ? hp / C5_HW - 1 : -(1 << 20);    // past the image: never a valid row
     sox[k] = hp % C5_HW - 1;
   }
-
-  // pixel index of each of this lane's slots for tile ti (-1: zero padding / past the image).  Recomputed
-  // per chunk (a few VALU per slot) rather than kept per tile: a per-tile array selected by tile parity was
-  // put in scratch, and scratch loads share vmcnt with the DMAs
-  auto geo = [&](int ti, int (&p)[DPW]) {
-    int n, h0, w0;
-    tile_of(ti, n, h0, w0);
-#pragma unroll
-    for (int k = 0; k < DPW; ++k) {
-      const int y = h0 + soy[k], x = w0 + sox[k];
-      p[k] = (sok[k] && (unsigned)y < (unsigned)d.H && (unsigned)x < (unsigned)d.W) ? (n * d.H + y) * d.W + x : -1;
-    }
-  };
+  constexpr int ND = DPW + WPW;   // DMA instructions per wave per chunk (without gate loads)
 
   // B-fragment byte offsets in a compute image: row r = wm*MI + rr (rr < MI+2), tap column dx
   unsigned xoff[3][MI + 2];
@@ -209,113 +185,147 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       xoff[dx][rr] = (unsigned)(2 * hp + ((lane >> 5) ^ ((hp >> 3) & 1))) * 16u;
     }
 
-  auto comp_buf = [&](int g) -> unsigned char* { return lds + Lay::OFF_COMP + (g % Lay::NCOMP) * Lay::IMG; };
-  auto raw_buf = [&](int g) -> unsigned char* { return lds + Lay::OFF_RAW + (g & 1) * Lay::IMG; };
-  auto w_buf = [&](int g) -> unsigned char* { return lds + Lay::OFF_W + (g % 3) * Lay::WIMG; };
+  // ring slots: compute images (PLAIN: 3 = chunk % 3; ACT: 2 = chunk & 1), raw images (ACT: chunk & 1),
+  // weights (chunk % 3), gate pre-activations (tile & 1)
+  auto comp_buf = [&](int slot) -> unsigned char* { return lds + Lay::OFF_COMP + slot * Lay::IMG; };
+  auto raw_buf = [&](int slot) -> unsigned char* { return lds + Lay::OFF_RAW + slot * Lay::IMG; };
+  auto w_buf = [&](int slot) -> unsigned char* { return lds + Lay::OFF_W + slot * Lay::WIMG; };
   auto gate_buf = [&](int ti) -> unsigned char* { return lds + Lay::OFF_GATE + (ti & 1) * Lay::GATE; };
+  // the same regions as LDS byte addresses (scalars) for the DMAs' M0
+  const unsigned l32 = lds_addr(lds);
+  const unsigned junk = l32 + Lay::OFF_JUNK;
 
-  // DMA of chunk step g (tile g / nch, channels 16 (g % nch) ..): halo slots, weight fragments, and at the
-  // tile's first chunk the gate pre-activations of this lane's slots; returns the instructions issued
-  auto issue = [&](int g) -> int {
-    const int ti = g / nch, c = g - ti * nch;
-    int p[DPW];
-    geo(ti, p);
-    const int cn0 = c * 16;
-    const int si = (d.nsrc > 1 && cn0 >= C0) ? 1 : 0;
-    const int cl = cn0 - (si ? C0 : 0);
-    const int Cs = si ? s1.C : C0;
-    const rsrc4_t rs = si ? rs1 : rs0;
-    unsigned char* dst = ACT ? raw_buf(g) : comp_buf(g);
-    int cnt = 0;
-    const bool abl_h = (ABL & 1) && g >= 2, abl_w = (ABL & 2) && g >= 2;
-#pragma unroll
-    for (int k = 0; k < DPW; ++k) {
-      const int i = wave + k * C5_NW;
-      if (i < NI && !abl_h) {
-        const int ch = cl + 8 * hbit[k];
-        const unsigned vo = (p[k] >= 0 && ch < Cs) ? ((unsigned)p[k] * (unsigned)Cs + (unsigned)ch) * 2u : OOB;
-        if (sok[k]) dma16(rs, dst + i * 1024, vo);
-        ++cnt;
-      }
+  // a chunk cursor: tile ti (origin n, h0, w0), 16-channel chunk c, ring slots of chunk index g
+  struct Cur {
+    int ti, c, n, h0, w0, s3, s2;
+  };
+  auto cur_init = [&](Cur& q) {
+    q.ti = 0; q.c = 0; q.s3 = 0; q.s2 = 0;
+    tile_of(0, q.n, q.h0, q.w0);
+  };
+  auto cur_next = [&](Cur& q) {
+    q.s3 = q.s3 == 2 ? 0 : q.s3 + 1;
+    q.s2 ^= 1;
+    if (++q.c == nch) {
+      q.c = 0;
+      if (++q.ti < ntl) tile_of(q.ti, q.n, q.h0, q.w0);
     }
-    unsigned char* wd = w_buf(g);
-#pragma unroll
-    for (int k = 0; k < WPW; ++k) {
-      const int j = wave + k * C5_NW;
-      if (j < 9 * C5_WN && !abl_w) {
-        const int tap = j >> 1, wj = j & 1;
-        const unsigned nt0 = (unsigned)((blockIdx.y * C5_BN + wj * 32) / 16);
-        dma16(rw, wd + j * 1024,
-              lanew + nt0 * jstride + (unsigned)((c >> 1) * 9 + tap) * 1024u + (unsigned)(c & 1) * 512u);
-        ++cnt;
-      }
-    }
-    if (gated && c == 0) {
+  };
+
+  // DMA of the chunk at cursor q: halo slots, weight fragments, and at a gated tile's first chunk the gate
+  // pre-activations of this lane's slots (returns whether those went out: the chunk counts ND + DPW)
+  auto issue = [&](const Cur& q, bool prologue) -> bool {
+    const int cn0 = q.c * 16;
+    const bool s1sel = d.nsrc > 1 && cn0 >= C0;
+    const int cl = s1sel ? cn0 - C0 : cn0;
+    const int Cs = s1sel ? s1.C : C0;
+    const rsrc4_t rs = s1sel ? rs1 : rs0;
+    const unsigned img = l32 + (ACT ? Lay::OFF_RAW + q.s2 * Lay::IMG : Lay::OFF_COMP + q.s3 * Lay::IMG);
+    const unsigned pbase = ((unsigned)q.n * d.H + q.h0) * d.W + q.w0;
+    if (!(ABL & 1) || prologue) {
 #pragma unroll
       for (int k = 0; k < DPW; ++k) {
         const int i = wave + k * C5_NW;
-        if (i < NI) {
-          if (sok[k]) dma4(rsg, gate_buf(ti) + i * 256, p[k] >= 0 ? (unsigned)p[k] * 4u : OOB);
-          ++cnt;
-        }
+        const int y = q.h0 + soy[k], x = q.w0 + sox[k], ch = cl + 8 * hbit[k];
+        const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W) & (ch < Cs);
+        const unsigned pix = pbase + (unsigned)(soy[k] * d.W + sox[k]);
+        dma16(rs, i < NI ? img + i * 1024 : junk, ok ? (pix * (unsigned)Cs + (unsigned)ch) * 2u : OOB);
       }
     }
-    return cnt;
+    if (!(ABL & 2) || prologue) {
+      const unsigned wd = l32 + Lay::OFF_W + q.s3 * Lay::WIMG;
+      const unsigned wofs = (unsigned)((q.c >> 1) * 9) * 1024u + (unsigned)(q.c & 1) * 512u;
+#pragma unroll
+      for (int k = 0; k < WPW; ++k) {
+        const int j = wave + k * C5_NW;
+        const int tap = j >> 1, wj = j & 1;
+        const unsigned nt0 = (unsigned)((blockIdx.y * C5_BN + wj * 32) / 16);
+        const unsigned vo = lanew + nt0 * jstride + (unsigned)tap * 1024u + wofs;
+        dma16(rw, j < 9 * C5_WN ? wd + j * 1024 : junk, j < 9 * C5_WN ? vo : OOB);
+      }
+    }
+    const bool gl = gated && q.c == 0;
+    if (gl) {
+      const unsigned gd = l32 + Lay::OFF_GATE + (q.ti & 1) * Lay::GATE;
+#pragma unroll
+      for (int k = 0; k < DPW; ++k) {
+        const int i = wave + k * C5_NW;
+        const int y = q.h0 + soy[k], x = q.w0 + sox[k];
+        const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
+        const unsigned pix = pbase + (unsigned)(soy[k] * d.W + sox[k]);
+        dma4(rsg, i < NI ? gd + i * 256 : junk, ok ? pix * 4u : OOB);
+      }
+    }
+    return gl;
   };
 
-  // BN-activation (+gate) transform of chunk step g, raw -> compute image, this lane's own DMA slots
-  auto transform = [&](int g) {
-    const int ti = g / nch, c = g - ti * nch;
-    int p[DPW];
-    geo(ti, p);
-    const int cn0 = c * 16;
+  // BN-activation (+gate) transform of the chunk at cursor q, raw -> compute image, this lane's own slots
+  // (zero-padding pixels and the image's tail slots come out 0)
+  auto transform = [&](const Cur& q) {
+    const int cn0 = q.c * 16;
     const bool act = !(d.nsrc > 1 && cn0 >= C0);    // src0 (activation) or src1 (stored: copied)
-    const unsigned char* rb = raw_buf(g);
-    unsigned char* cb = comp_buf(g);
+    const unsigned char* rb = raw_buf(q.s2);
+    unsigned char* cb = comp_buf(q.s2);
     const float* tab = reinterpret_cast<const float*>(lds + Lay::OFF_TAB);
 #pragma unroll
     for (int k = 0; k < DPW; ++k) {
       const int i = wave + k * C5_NW;
-      if (i < NI && sok[k]) {
+      if (i < NI) {
         const int s = i * 64 + lane;
-        uint4 q = *reinterpret_cast<const uint4*>(rb + s * 16);
+        uint4 q4 = *reinterpret_cast<const uint4*>(rb + s * 16);
         if (act) {
-          const int ch = cn0 + 8 * hbit[k];
-          const bool ok = p[k] >= 0 && ch < C0;
-          const float4 a0 = *reinterpret_cast<const float4*>(tab + (ok ? ch : 0));
-          const float4 a1 = *reinterpret_cast<const float4*>(tab + (ok ? ch : 0) + 4);
-          const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_CMAX + (ok ? ch : 0));
-          const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_CMAX + (ok ? ch : 0) + 4);
+          const int y = q.h0 + soy[k], x = q.w0 + sox[k], ch = cn0 + 8 * hbit[k];
+          const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W) & (ch < C0);
+          const int cc = ok ? ch : 0;
+          const float4 a0 = *reinterpret_cast<const float4*>(tab + cc);
+          const float4 a1 = *reinterpret_cast<const float4*>(tab + cc + 4);
+          const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_CMAX + cc);
+          const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_CMAX + cc + 4);
           const float sc[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
           const float sf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
           float gm = ok ? 1.f : 0.f;
           if (gated) {
-            const float pv = *reinterpret_cast<const float*>(gate_buf(ti) + i * 256 + lane * 4);
+            const float pv = *reinterpret_cast<const float*>(gate_buf(q.ti) + i * 256 + lane * 4);
             gm = ok ? sigmoidf_(pv * ga + gb) : 0.f;
           }
           float v[8];
-          unpack8_16<T>(q, v);
+          unpack8_16<T>(q4, v);
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo) * gm;
-          q = pack8_16<T>(v);
+          q4 = pack8_16<T>(v);
         }
-        *reinterpret_cast<uint4*>(cb + s * 16) = q;
+        *reinterpret_cast<uint4*>(cb + s * 16) = q4;
       }
     }
   };
 
-  // ---- prologue: scale/shift table, chunks 0 and 1 in flight, chunk 0 ready ----
+  // ---- prologue: scale/shift table, chunks 0-2 in flight, chunk 0 ready ----
   if constexpr (ACT) {
     float* tab = reinterpret_cast<float*>(lds + Lay::OFF_TAB);
     for (int c = tid; c < C0; c += C5_NT) { tab[c] = s0.scale[c]; tab[C5_CMAX + c] = s0.shift[c]; }
     if (tid < 8) { tab[C0 + tid] = 0.f; tab[C5_CMAX + C0 + tid] = 0.f; }
   }
-  issue(0);
-  if (G > 1) issue(1);
-  wait_vm<0>();
+  // cursors: I = the next chunk to DMA, X = the next chunk to transform (ACT), K = the chunk being computed.
+  // G >= 2 (nch >= 2).  The youngest DMA'd chunk's instruction count decides each wait: ND, ND + DPW (gate
+  // loads went out with it) or none in flight (0).
+  Cur I, X, K;
+  cur_init(I);
+  cur_init(K);
+  issue(I, true);
+  cur_next(I);
+  issue(I, true);           // chunk 1: never a tile's first chunk (nch >= 2)
+  cur_next(I);
+  wait_vm<ND>();            // chunk 0 landed
   if constexpr (ACT) {
-    lds_barrier();      // the scale/shift table
-    transform(0);
+    lds_barrier();          // the scale/shift table
+    cur_init(X);
+    transform(X);           // chunk 0; then chunk 2 may reuse its raw slot
+    cur_next(X);
+  }
+  bool y_live = G > 2, y_big = false;
+  if (y_live) {
+    y_big = issue(I, true);
+    cur_next(I);
   }
   lds_barrier();
 
@@ -326,36 +336,63 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   for (int r = 0; r < 16; ++r) { sA[r] = 0.f; sB[r] = 0.f; }
   f32x16 acc[MI];
 
-  int g = 0;
+  // operand fragments of one tap column dx of the chunk at K: MI+2 halo rows (B) and the 3 taps' weights (A)
+  auto load_col = [&](const Cur& q, int dx, F (&x)[MI + 2], F (&w)[3]) {
+    const unsigned char* xb = comp_buf(ACT ? q.s2 : q.s3);
+    const unsigned char* wb = w_buf(q.s3) + wn * 1024 + lane * 16;
+#pragma unroll
+    for (int rr = 0; rr < MI + 2; ++rr) x[rr] = *reinterpret_cast<const F*>(xb + xoff[dx][rr]);
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const F*>(wb + (dy * 3 + dx) * 2048);
+  };
+  auto mma_col = [&](const F (&x)[MI + 2], const F (&w)[3]) {
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[i] = Mma32<T>::mma(w[dy], x[i + dy], acc[i]);
+  };
+  // this wave's DMAs of the chunk after K have landed: only the youngest chunk's may still be in flight
+  auto wait_next = [&]() {
+    if (!y_live) wait_vm<0>();
+    else if (y_big) wait_vm<ND + DPW>();
+    else wait_vm<ND>();
+  };
+  auto issue_next = [&]() {
+    // called right after a chunk's barrier: every wave has finished reading chunk K, whose ring slots
+    // the DMA of chunk K+3 (the cursor I) reuses
+    y_live = I.ti < ntl;
+    if (y_live) {
+      y_big = issue(I, false);
+      cur_next(I);
+    }
+  };
+
+  F xA[MI + 2], wA[3], xB[MI + 2], wB[3];
   for (int ti = 0; ti < ntl; ++ti) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
 #pragma unroll 1
-    for (int c = 0; c < nch; ++c, ++g) {
-      const int nd = (g + 2 < G) ? issue(g + 2) : 0;
-      const unsigned char* xb = comp_buf(g);
-      const unsigned char* wb = w_buf(g) + wn * 1024 + lane * 16;
-      F xr[MI + 2];
-#pragma unroll
-      for (int st = 0; st < 9; ++st) {
-        const int dx = st / 3, dy = st % 3, t = dy * 3 + dx;
-        if (dy == 0) {
-#pragma unroll
-          for (int rr = 0; rr < MI + 2; ++rr) xr[rr] = *reinterpret_cast<const F*>(xb + xoff[dx][rr]);
-        }
-        const F a = *reinterpret_cast<const F*>(wb + t * 2048);
-#pragma unroll
-        for (int i = 0; i < MI; ++i) acc[i] = Mma32<T>::mma(a, xr[i + dy], acc[i]);
-        if (st == 4) {
-          wait_vm_n(nd);                 // this wave's DMAs of step g+1 (issued one step ago) have landed
-          if constexpr (ACT && !(ABL & 16)) {
-            if (g + 1 < G) transform(g + 1);
-          }
+    for (int c = 0; c < nch; ++c) {
+      // one tap column at a time; the barrier ends the chunk (after it: chunk K's slots are free and the
+      // next chunk is readable by every wave)
+      load_col(K, 0, xA, wA);
+      mma_col(xA, wA);
+      load_col(K, 1, xB, wB);
+      mma_col(xB, wB);
+      wait_next();
+      if constexpr (ACT && !(ABL & 16)) {
+        if (X.ti < ntl) {
+          transform(X);
+          cur_next(X);
         }
       }
+      load_col(K, 2, xA, wA);
+      mma_col(xA, wA);
       if constexpr (!(ABL & 8)) lds_barrier();
+      issue_next();
+      cur_next(K);
     }
 
     // ---------------- epilogue of tile ti ----------------
@@ -562,10 +599,10 @@ static int conv5_gx(const unet_conv_desc* d) {
 bool conv5_eligible(const unet_conv_desc* d) {
   const int mode = conv5_mode();
   if (mode == 0) return false;
-  // default: the 16-bit y outputs of <= 64 channels (the 512^2 / 256^2 encoder-decoder ends), where
-  // conv5 measured 10-25 % faster than conv3 (profiles/r03_layerprof_*.txt); conv3 keeps the wider
-  // layers and the fp32 dgrads, where its 16x16x32 tiles over the full Cout measured faster
-  if (mode == 2 && (d->Cout > C5_BN || d->out_mode != UNET_OUT_Y)) return false;
+  // default: every 16-bit y output (forward and the middle-activation dgrads) and the fp32 dgrads of <= 64
+  // channels — per layer conv5 measured 0-31 % faster there (the 512^2 64-channel layers 14-31 %); the
+  // wider fp32 dgrads stay on conv3, whose tiles measured 5-20 % faster (profiles/r03_layerprof_*.txt)
+  if (mode == 2 && d->out_mode == UNET_OUT_F32 && d->Cout > C5_BN) return false;
   if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 3) return false;
   if (d->out_mode != UNET_OUT_Y && d->out_mode != UNET_OUT_F32) return false;
   if (d->Cout % 8 || (d->out_mode == UNET_OUT_F32 && d->split % 4)) return false;   // 16-byte y stores
