@@ -153,6 +153,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   const unsigned jstride = (unsigned)nch32 * 9u * 1024u;
   const unsigned ntiles16 = (unsigned)((d.Cout + C5_NPAD - 1) / C5_NPAD * (C5_NPAD / 16));
   const rsrc4_t rw = mk_rsrc4(d.weight, ntiles16 * jstride);
+  const rsrc_t ry = mk_rsrc(d.out, (unsigned)(npix * d.Cout * 2));   // y output (OM5_Y)
   const unsigned lanew = (unsigned)((lane >> 4) & 1) * jstride + (unsigned)(16 * (lane >> 5) + (lane & 15)) * 16u;
 
   // ---- this lane's halo DMA slots: instruction i = wave + k*NW covers slots 64 i .. 64 i + 63 ----
@@ -352,10 +353,19 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       for (int i = 0; i < MI; ++i) acc[i] = Mma32<T>::mma(w[dy], x[i + dy], acc[i]);
   };
   // this wave's DMAs of the chunk after K have landed: only the youngest chunk's may still be in flight
+  // (the y epilogue's NST stores sit between DMA batches for the two chunks after it: sw counts them down)
+  constexpr int NST = OM == OM5_Y ? 2 * MI : 0;
+  int sw = 0;
   auto wait_next = [&]() {
     if (!y_live) wait_vm<0>();
-    else if (y_big) wait_vm<ND + DPW>();
-    else wait_vm<ND>();
+    else if (NST && sw > 0) {
+      if (y_big) wait_vm<ND + DPW + NST>();
+      else wait_vm<ND + NST>();
+    } else {
+      if (y_big) wait_vm<ND + DPW>();
+      else wait_vm<ND>();
+    }
+    if (NST && sw > 0) --sw;
   };
   auto issue_next = [&]() {
     // called right after a chunk's barrier: every wave has finished reading chunk K, whose ring slots
@@ -413,7 +423,6 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     rows = rows < 0 ? 0 : (rows > MI ? MI : rows);
     const unsigned pix0 = ((unsigned)n * d.H + oh0) * (unsigned)d.W + ow;
     if constexpr (OM == OM5_Y) {
-      T* y = (T*)d.out;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const bool ok = colok && i < rows;
@@ -421,6 +430,8 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
         // lane l < 32 holds channels 8gq+0..3 of pixel l, lane l+32 channels 8gq+4..7 of the same pixel:
         // v_permlane32_swap of the packed groups (gq, gq+1) leaves lanes 0-31 with channels 8gq..8gq+7 and
         // lanes 32-63 with 8gq+8..8gq+15 — one 16-byte store per pair instead of two 8-byte ones
+        // Buffer stores with out-of-range offsets for the masked lanes: every wave issues exactly NST stores
+        // per tile (no exec branch), which the next chunks' vmcnt waits count (wait_next)
         unsigned px_[4], py_[4];
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
@@ -432,10 +443,13 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
           const auto sx = __builtin_amdgcn_permlane32_swap(px_[kp], px_[kp + 1], false, false);
           const auto sy = __builtin_amdgcn_permlane32_swap(py_[kp], py_[kp + 1], false, false);
           const int co = cw0 + 8 * kp + 8 * hh;
-          if (ok && co < d.Cout)
-            *reinterpret_cast<uint4*>(y + (size_t)pix * d.Cout + co) = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          const unsigned vo = (ok && co < d.Cout) ? (pix * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
+          typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+          const u32x4 v4 = {sx[0], sy[0], sx[1], sy[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(v4, ry, (int)vo, 0, 0);
         }
       }
+      sw = 2;
       if (d.stats) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
@@ -619,6 +633,7 @@ bool conv5_eligible(const unet_conv_desc* d) {
     if (s.H != d->H || s.W != d->W) return false;
   }
   if ((double)d->N * d->H * d->W * 4 >= (double)OOB) return false;
+  if ((double)d->N * d->H * d->W * d->Cout * 2 >= (double)OOB) return false;   // y stores: OOB masks lanes
   const long long work = conv5_mtiles(d) * cdiv(d->Cout, C5_BN);
   return work >= 256;
 }
