@@ -134,7 +134,7 @@ def _hbm_bytes(name: str, a: tuple):
         d = a[0]
         v = conv_kernel_name(d)
         fam = v.split("<")[0]
-        if fam not in ("smallcin_fwd_kernel", "pw_conv_kernel"):
+        if fam not in ("smallcin_fwd_kernel", "smallcin_fwd_mfma_kernel", "pw_conv_kernel"):
             return None
         P = d.N * d.H * d.W
         rd = sum(P * d.src[i].C * (4 if d.src[i].kind == 4 else _es(d.dtype)) for i in range(d.nsrc))
@@ -224,6 +224,8 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-fp32-line", action="store_true",
                     help="skip the fp32-operand (reference numerics) rate reported beside a 16-bit run at N=1")
+    ap.add_argument("--no-graph-line", action="store_true",
+                    help="skip the HIP-graph replay rate of the same step reported beside the eager one at N=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -298,6 +300,8 @@ def main():
     for _ in range(args.warmup):
         step()
     elapsed, loss = timed(step, args.steps)          # the headline: no probe events inside
+    final_loss = round(float(loss.detach()), 5)
+    del loss     # the last step's autograd graph (its AccumulateGrad nodes) must not outlive the step
 
     # the dominant kernel family, timed live in a separate pass of the same steps: every 16-bit 3x3 conv
     # launch (fwd + dgrad; the 32x32x16-MFMA conv5_kernel / conv4_kernel tiles on the large maps and the
@@ -370,13 +374,26 @@ def main():
                 "note": "algorithmic bytes (each operand read once, each output written once) / HIP-event time "
                         "per launch, separate pass; measured_bytes_per_launch: rocprofv3 FETCH_SIZE x2 + "
                         "WRITE_SIZE (profiles/traffic.json)"},
-        "final_loss": round(float(loss.detach()), 5),
+        "final_loss": final_loss,
         "without_optimizer": {"value": round(world * args.batch * args.accum * args.steps / el_nb, 3),
                               "ms_per_step": round(el_nb / args.steps * 1e3, 3),
                               "note": "fwd+DiceBCE+bwd (+grad averaging), no clip/AdamW"},
     }
     if scaler.is_enabled():
         line["loss_scale"] = float(scaler.get_scale())
+    if world == 1 and args.accum == 1 and not scaler.is_enabled() and not args.no_graph_line:
+        # the same step (fwd + DiceBCE + bwd + clip + AdamW) captured once as a HIP graph and replayed
+        # (unet.utils.graphed.GraphedTrainStep): identical kernels, one host launch per step
+        from unet.utils.graphed import GraphedTrainStep
+        gopt = torch.optim.AdamW(model.parameters(), lr=5e-5, weight_decay=1e-4, fused=True, capturable=True)
+        gs = GraphedTrainStep(model, crit, gopt, x.shape, t.shape, target_dtype=t.dtype, clip_norm=1.0)
+        for _ in range(3):
+            gs(x, t)
+        elg, _ = timed(lambda: gs(x, t), args.steps)
+        line["graphed_step"] = {"value": round(args.batch * args.steps / elg, 3),
+                                "ms_per_step": round(elg / args.steps * 1e3, 3),
+                                "note": "same train step replayed as one HIP graph (GraphedTrainStep)"}
+        del gs, gopt
     if world == 1 and args.precision != "fp32" and not args.no_fp32_line:
         # the same step with fp32 operands (the reference's numerics; what the parity tests pin)
         model.hip_precision = "fp32"

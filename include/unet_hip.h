@@ -127,6 +127,8 @@ int unet_conv_mtiles(int N, int H, int W);
 int unet_conv_stats_rows(const unet_conv_desc* d);
 /* name of the kernel instantiation unet_conv dispatches d to (for profiling / roofline probes)   */
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len);
+/* name of the weight-gradient kernel unet_conv_wgrad dispatches d to (profiling / tests)          */
+int unet_wgrad_variant(const unet_wgrad_desc* d, char* buf, int len);
 
 /* ---- weights (nn.Conv2d weight OIHW fp32 -> packed operand) -------------------------------- */
 /* replaces the implicit weight read of nn.Conv2d — layers.py:32,35,120,152,158,164            */

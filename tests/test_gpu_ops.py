@@ -211,9 +211,11 @@ def test_conv_wgrad(prec, shape, k, kind):
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16", "fp32"])
-@pytest.mark.parametrize("shape", [(2, 1, 40, 36, 64), (1, 3, 33, 50, 16), (4, 1, 64, 64, 8)])
+@pytest.mark.parametrize("shape", [(2, 1, 40, 36, 64), (1, 3, 33, 50, 16), (4, 1, 64, 64, 8),
+                                   (2, 3, 70, 100, 64), (4, 1, 512, 512, 64), (1, 2, 9, 130, 64)])
 def test_first_conv_nchw_input(prec, shape):
-    """inc.0: the fp32 NCHW model input read directly (csrc/smallcin.hip), fwd + BN sums + wgrad."""
+    """inc.0: the fp32 NCHW model input read directly (csrc/smallcin.hip), fwd + BN sums + wgrad.  16-bit,
+    64 output channels: the MFMA forward (x split into two 16-bit halves); otherwise the VALU kernel."""
     L, R = _lib(), _rt()
     P = R._PRECISIONS[prec]
     N, cin, H, W, cout = shape
@@ -233,6 +235,8 @@ def test_first_conv_nchw_input(prec, shape):
     d.weight, d.out_mode, d.out, d.stats = wp.data_ptr(), L.OUT_Y, out.data_ptr(), st.data_ptr()
     L.call("unet_conv", d, R.stream())
     torch.cuda.synchronize()
+    want = "smallcin_fwd_mfma_kernel" if prec != "fp32" and cout == 64 else "smallcin_fwd_kernel"
+    assert _variant(d).startswith(want), _variant(d)
     xr = x.to(dt).float() if prec != "fp32" else x
     ref = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)
     tol = 1e-2 if prec != "fp32" else 1e-5

@@ -14,7 +14,7 @@ sys.path.insert(0, str(ROOT / "unet-segment-pytorch_amd"))
 import torch  # noqa: E402
 
 from unet._hip import lib as L  # noqa: E402
-from unet._hip.runtime import conv_kernel_name  # noqa: E402
+from unet._hip.runtime import conv_kernel_name, wgrad_kernel_name  # noqa: E402
 
 KIND = {0: "plain", 1: "act", 2: "pool", 3: "up", 4: "nchw", 5: "upplain"}
 OUT = {0: "y", 1: "f32", 2: "poolbwd", 3: "shuf2", 4: "f32gate"}
@@ -32,7 +32,7 @@ def _desc_info(name, d):
         var = conv_kernel_name(d)
     else:
         tag = "wgrad       "
-        var = ""
+        var = wgrad_kernel_name(d)
     return f"{tag} {d.N}x{d.H}x{d.W} {d.Cin:4d}->{d.Cout:4d} k{d.ksize} [{srcs}] {var}", fl
 
 

@@ -497,6 +497,8 @@ int pw_conv_rows(const unet_conv_desc* d);
 int pw_conv(const unet_conv_desc* d, hipStream_t st);
 int pw_conv_variant(const unet_conv_desc* d, char* buf, int len);
 int smallcin_rows(long long P);
+int smallcin_stats_rows(const unet_conv_desc* d);
+bool smallcin_is_mfma(const unet_conv_desc* d);
 int smallcin_conv(const unet_conv_desc* d, hipStream_t st);
 
 // the pipelined kernel needs every source channel vector to be one aligned 16-byte load, and every
@@ -611,7 +613,7 @@ static bool bnb_in_epilogue(const unet_conv_desc* d) {
 
 int unet_conv_stats_rows(const unet_conv_desc* d) {
   if (d->bnb_y && !bnb_in_epilogue(d)) return unet_bn_bwd_reduce_rows((long long)d->N * d->H * d->W, d->Cout);
-  if (smallcin_conv_ok(d)) return smallcin_rows((long long)d->N * d->H * d->W);
+  if (smallcin_conv_ok(d)) return smallcin_stats_rows(d);
   if (pw_conv_ok(d)) return pw_conv_rows(d);
   if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
   if (conv5_eligible(d)) return conv5_stats_rows(d);
@@ -622,7 +624,7 @@ int unet_conv_stats_rows(const unet_conv_desc* d) {
 
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
   if (smallcin_conv_ok(d)) {
-    snprintf(buf, len, "smallcin_fwd_kernel<%s>", tname(d->dtype));
+    snprintf(buf, len, smallcin_is_mfma(d) ? "smallcin_fwd_mfma_kernel<%s>" : "smallcin_fwd_kernel<%s>", tname(d->dtype));
     return 0;
   }
   if (pw_conv_ok(d)) return pw_conv_variant(d, buf, len);

@@ -6,7 +6,7 @@
 // L1-cached input taps and writes them as one 16-byte vector, plus BN partial sums.  Weight
 // gradient: per-thread 8 x (9*Cin) partial sums over a pixel range, reduced across the block, one
 // fp32 row per block; unet_colsum finishes (fixed order).
-#include "common.h"
+#include "conv_src16.h"
 
 namespace unet {
 
@@ -295,7 +295,151 @@ __global__ __launch_bounds__(256) void smallcin_wgrad_kernel(const unet_wgrad_de
   }
 }
 
+// 16-bit output, Cout = 64, Cin <= 3: the layer on MFMA.  y[co][px] = Σ_k W[co][k] X[k][px] with
+// K = [the 9 Cin taps of x_hi | the same taps of x_lo] (x = x_hi + x_lo, both 16-bit, so the fp32 input keeps
+// ~17 mantissa bits; weights are the 16-bit packed ones), padded to 32 / 64 with zeros: one or two
+// v_mfma_f32_16x16x32 per 16 output channels x 16 pixels.  The fp32 NCHW input tile (+ halo) is staged in LDS
+// by coalesced loads; a wave owns 16 pixels of each tile row and writes 4 channels x 16 bit per lane and
+// fragment; BN partial sums of the fp32 accumulators per wave.  The VALU kernel above is issue-bound at
+// ~4x the HBM time of its 67 MB output (profiles/r01_smallcin_pmc.txt).
+template <typename T> struct SCElem;
+template <> struct SCElem<bf16> { typedef __bf16 type; };
+template <> struct SCElem<f16> { typedef _Float16 type; };
+constexpr int SCM_TR = 8, SCM_TW = 64, SCM_HW = SCM_TW + 2;
+constexpr int SCM_GRID = 512;     // persistent blocks; stats rows = 4 per block
+
+template <typename T>
+__global__ __launch_bounds__(256) void smallcin_fwd_mfma_kernel(const unet_conv_desc d, int ntiles) {
+  using F = typename Mma<T>::frag;
+  __shared__ float xt[4 * (SCM_TR + 2) * SCM_HW];   // [ci][row][col] fp32 input tile with halo
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int Cin = d.Cin, K9 = 9 * Cin, nks = (2 * K9 + 31) / 32;
+  const int tiles_w = (d.W + SCM_TW - 1) / SCM_TW, tiles_h = (d.H + SCM_TR - 1) / SCM_TR;
+  const float* x = (const float*)d.src[0].data;
+  const int Cs = d.src[0].C;
+  const T* wp = (const T*)d.weight;
+  // A fragments (weights): lane holds W[co = 16 f + c16][k = 32 ks + 8 g + e]; B operand offsets: the LDS
+  // element of k = 32 ks + 8 g + e relative to the lane's pixel (-1: zero), and whether it is the low half
+  F a[2][4];
+  int off[2][8];
+  unsigned lomask = 0;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 32 * ks + 8 * g + e;
+      const bool real = k < 2 * K9;
+      const int kk = k < K9 ? k : k - K9;
+      const int ci = kk / 9, tap = kk % 9;
+      off[ks][e] = real ? ci * (SCM_TR + 2) * SCM_HW + (tap / 3) * SCM_HW + tap % 3 : -1;
+      if (real && k >= K9) lomask |= 1u << (8 * ks + e);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const float wv = real ? packed_w<T>(wp, 16 * f + c16, ci, tap, 1) : 0.f;
+        a[ks][f][e] = (typename SCElem<T>::type)wv;
+      }
+    }
+  float s1[4][4], s2[4][4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[f][r] = 0.f; s2[f][r] = 0.f; }
+  T* y = (T*)d.out;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tw = tile % tiles_w, t2 = tile / tiles_w;
+    const int h0 = (t2 % tiles_h) * SCM_TR, w0 = tw * SCM_TW, n = t2 / tiles_h;
+    __syncthreads();
+    const int nel = Cin * (SCM_TR + 2) * SCM_HW;
+    for (int i = tid; i < nel; i += 256) {
+      const int ci = i / ((SCM_TR + 2) * SCM_HW), rem = i % ((SCM_TR + 2) * SCM_HW);
+      const int yy = h0 - 1 + rem / SCM_HW, xx = w0 - 1 + rem % SCM_HW;
+      xt[i] = ((unsigned)yy < (unsigned)d.H && (unsigned)xx < (unsigned)d.W)
+                  ? x[(((size_t)n * Cs + ci) * d.H + yy) * d.W + xx] : 0.f;
+    }
+    __syncthreads();
+    const int ow = w0 + 16 * wave + c16;
+    for (int r = 0; r < SCM_TR && h0 + r < d.H; ++r) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* xr = xt + r * SCM_HW + 16 * wave + c16;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks < nks) {
+          F b;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = off[ks][e] >= 0 ? xr[off[ks][e] < 0 ? 0 : off[ks][e]] : 0.f;
+            const float hi = (float)(typename SCElem<T>::type)v;
+            b[e] = (typename SCElem<T>::type)(((lomask >> (8 * ks + e)) & 1) ? v - hi : v);
+          }
+#pragma unroll
+          for (int f = 0; f < 4; ++f) acc[f] = Mma<T>::mma(a[ks][f], b, acc[f]);
+        }
+      }
+      if (ow < d.W) {
+        const size_t pix = ((size_t)n * d.H + h0 + r) * d.W + ow;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          uint2 pk;
+          pk.x = pack2_16<T>(acc[f][0], acc[f][1]);
+          pk.y = pack2_16<T>(acc[f][2], acc[f][3]);
+          *reinterpret_cast<uint2*>(y + pix * 64 + 16 * f + 4 * g) = pk;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            s1[f][q] += acc[f][q];
+            s2[f][q] = __builtin_fmaf(acc[f][q], acc[f][q], s2[f][q]);
+          }
+        }
+      }
+    }
+  }
+  if (!d.stats) return;
+  const int rows = gridDim.x * 4, row = blockIdx.x * 4 + wave;
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float a1 = row16_sum(s1[f][q]), a2 = row16_sum(s2[f][q]);
+      if (c16 == 0) {
+        const int co = 16 * f + 4 * g + q;
+        d.stats[(size_t)co * rows + row] = a1;
+        d.stats[((size_t)64 + co) * rows + row] = a2;
+      }
+    }
+}
+
+static bool smallcin_mfma_ok(const unet_conv_desc* d) {
+  const char* e = getenv("UNET_SMALLCIN_MFMA");
+  if (e && !atoi(e)) return false;
+  return (d->dtype == UNET_BF16 || d->dtype == UNET_F16) && d->Cout == 64 && d->Cin <= 3;
+}
+
+static int smallcin_mfma_tiles(const unet_conv_desc* d) {
+  return d->N * cdiv(d->H, SCM_TR) * cdiv(d->W, SCM_TW);
+}
+
+int smallcin_stats_rows(const unet_conv_desc* d) {
+  if (smallcin_mfma_ok(d)) {
+    const int t = smallcin_mfma_tiles(d);
+    return 4 * (t < SCM_GRID ? t : SCM_GRID);
+  }
+  return smallcin_rows((long long)d->N * d->H * d->W);
+}
+
+bool smallcin_is_mfma(const unet_conv_desc* d) { return smallcin_mfma_ok(d); }
+
 int smallcin_conv(const unet_conv_desc* d, hipStream_t st) {
+  if (smallcin_mfma_ok(d)) {
+    const int t = smallcin_mfma_tiles(d);
+    const int grid = t < SCM_GRID ? t : SCM_GRID;
+    if (d->dtype == UNET_BF16)
+      hipLaunchKernelGGL(smallcin_fwd_mfma_kernel<bf16>, dim3(grid), dim3(256), 0, st, *d, t);
+    else
+      hipLaunchKernelGGL(smallcin_fwd_mfma_kernel<f16>, dim3(grid), dim3(256), 0, st, *d, t);
+    return check_launch("smallcin_fwd_mfma");
+  }
   if (d->Cout > 64) { set_error("smallcin: Cout > 64"); return UNET_ERR_UNSUPPORTED; }
   const int rows = smallcin_rows((long long)d->N * d->H * d->W);
   if (d->dtype == UNET_BF16)
@@ -307,11 +451,185 @@ int smallcin_conv(const unet_conv_desc* d, hipStream_t st) {
   return check_launch("smallcin_fwd");
 }
 
+// weight gradient on MFMA (16-bit dy, Cout = 64, Cin <= 3): D[co][k] = Σ_px dy[px][co] X[px][k], K = the
+// pixels (32 per v_mfma_f32_16x16x32, one tile-row half), k = [the 9 Cin taps of x_hi | the same of x_lo]
+// (16 per fragment); dW[co][ci][tap] = D[co][k] + D[co][k + 9 Cin] (smallcin_fold).  A wave stages the dy of
+// its 32 pixels (4 KB, one coalesced 16-byte load per lane x 4, prefetched one step ahead) in its own LDS
+// slice, swizzled for the conflict-free transposed reads (ds_read_b64_tr_b16) that turn NHWC pixel rows into
+// K-major fragments; the fp32 input tile is shared by the block.  Per-wave partial D rows, fixed-order sums.
+template <typename T>
+__global__ __launch_bounds__(256) void smallcin_wgrad_mfma_kernel(const unet_wgrad_desc d, int ntiles, float* part) {
+  using F = typename Mma<T>::frag;
+  __shared__ float xt[4 * (SCM_TR + 2) * SCM_HW];
+  __shared__ __attribute__((aligned(16))) unsigned char dyl[4][32 * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15, q = (lane >> 2) & 3, pp = lane & 3;
+  const int Cin = d.Cin, K9 = 9 * Cin, NJ = (2 * K9 + 15) / 16;
+  const int tiles_w = (d.W + SCM_TW - 1) / SCM_TW, tiles_h = (d.H + SCM_TR - 1) / SCM_TR;
+  const float* x = (const float*)d.src[0].data;
+  const int Cs = d.src[0].C;
+  const rsrc_t rdy = mk_rsrc(d.dy, (unsigned)((long long)d.N * d.H * d.W * 128));
+  // B operand: lane's k = 16 j + c16 -> LDS element offset of its tap (-1: zero column) and hi / lo half
+  int boff[4];
+  unsigned lom = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = 16 * j + c16;
+    const bool real = k < 2 * K9;
+    const int kk = k < K9 ? k : k - K9;
+    const int ci = kk / 9, tap = kk % 9;
+    boff[j] = real ? ci * (SCM_TR + 2) * SCM_HW + (tap / 3) * SCM_HW + tap % 3 : -1;
+    if (real && k >= K9) lom |= 1u << j;
+  }
+  // A operand (dy, 16 co x 32 px): transposed-read addresses in the wave's swizzled dy slice
+  // (pixel px = 128 B = 8 units of 8 channels, unit u stored at u ^ swz(px), swz as wgrad5's UPP = 8)
+  auto swz = [](int px) { return 2 * ((px >> 1) & 1) + 4 * ((px >> 3) & 1); };
+  unsigned aoff[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int px = 8 * g + 4 * h + q, u = 2 * f + (pp >> 1);
+      aoff[h][f] = (unsigned)(px * 128 + ((u ^ swz(px)) * 16) + 8 * (pp & 1));
+    }
+  // this lane's 4 staged dy units: pixel 8 k + (lane >> 3), unit lane & 7
+  unsigned woff[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int px = 8 * k + (lane >> 3), u = lane & 7;
+    woff[k] = (unsigned)(px * 128 + ((u ^ swz(px)) * 16));
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  unsigned char* dw_ = dyl[wave];
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tw = tile % tiles_w, t2 = tile / tiles_w;
+    const int h0 = (t2 % tiles_h) * SCM_TR, w0 = tw * SCM_TW, n = t2 / tiles_h;
+    __syncthreads();
+    const int nel = Cin * (SCM_TR + 2) * SCM_HW;
+    for (int i = tid; i < nel; i += 256) {
+      const int ci = i / ((SCM_TR + 2) * SCM_HW), rem = i % ((SCM_TR + 2) * SCM_HW);
+      const int yy = h0 - 1 + rem / SCM_HW, xx = w0 - 1 + rem % SCM_HW;
+      xt[i] = ((unsigned)yy < (unsigned)d.H && (unsigned)xx < (unsigned)d.W)
+                  ? x[(((size_t)n * Cs + ci) * d.H + yy) * d.W + xx] : 0.f;
+    }
+    __syncthreads();
+    // K steps of this wave: rows wave, wave + 4; two 32-pixel halves each
+    uint4 nx[4];
+    auto load_dy = [&](int st) {
+      const int r = wave + 4 * (st >> 1), c0 = 32 * (st & 1);
+      const int oh = h0 + r;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ow = w0 + c0 + 8 * k + (lane >> 3);
+        const bool ok = oh < d.H && ow < d.W;
+        const unsigned pix = ((unsigned)n * d.H + oh) * (unsigned)d.W + ow;
+        nx[k] = bld(rdy, ok ? pix * 128u + (unsigned)(lane & 7) * 16u : OOB, 0);
+      }
+    };
+    load_dy(0);
+#pragma unroll 1
+    for (int st = 0; st < 4; ++st) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(dw_ + woff[k]) = nx[k];
+      if (st + 1 < 4) load_dy(st + 1);
+      F a[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const i16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(dw_ + aoff[0][f]));
+        const i16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4*)(dw_ + aoff[1][f]));
+        a[f] = __builtin_bit_cast(F, __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      const int r = wave + 4 * (st >> 1), c0 = 32 * (st & 1);
+      const float* xr = xt + r * SCM_HW + c0 + 8 * g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < NJ) {
+          F b;
+          const int o = boff[j] < 0 ? 0 : boff[j];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = boff[j] >= 0 ? xr[o + e] : 0.f;
+            const float hi = (float)(typename SCElem<T>::type)v;
+            b[e] = (typename SCElem<T>::type)(((lom >> j) & 1) ? v - hi : v);
+          }
+#pragma unroll
+          for (int f = 0; f < 4; ++f) acc[f][j] = Mma<T>::mma(a[f], b, acc[f][j]);
+        }
+      }
+    }
+  }
+  // partial D of this wave: part[row][co][k] (k < 2 K9), row = 4 * block + wave
+  const int row = blockIdx.x * 4 + wave, K2 = 2 * K9;
+  float* pr = part + (size_t)row * 64 * K2;
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 16 * j + c16;
+      if (j < NJ && k < K2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pr[(16 * f + 4 * g + r) * K2 + k] = acc[f][j][r];
+      }
+    }
+}
+
+// dW[co][kk] (+)= Σ_rows part[row][co][kk] + part[row][co][kk + K9]  (fixed order)
+__global__ void smallcin_fold_kernel(const float* part, int rows, int Cout, int K9, float* dw, int accum) {
+  __shared__ float red[256];
+  const int col = blockIdx.x, co = col / K9, kk = col % K9, K2 = 2 * K9;
+  float s = 0.f;
+  for (int r = threadIdx.x; r < rows; r += 256) {
+    const float* p = part + ((size_t)r * Cout + co) * K2;
+    s += p[kk] + p[kk + K9];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dw[col] = accum ? dw[col] + red[0] : red[0];
+}
+
+static bool smallcin_wgrad_mfma_ok(const unet_wgrad_desc* d) {
+  const char* e = getenv("UNET_SMALLCIN_MFMA");
+  if (e && !atoi(e)) return false;
+  return (d->dtype == UNET_BF16 || d->dtype == UNET_F16) && d->Cout == 64 && d->Cin <= 3 &&
+         (double)d->N * d->H * d->W * 128 < (double)OOB;
+}
+
+static int smallcin_wgrad_grid(const unet_wgrad_desc* d, int* tiles) {
+  const int t = d->N * cdiv(d->H, SCM_TR) * cdiv(d->W, SCM_TW);
+  if (tiles) *tiles = t;
+  return t < SCM_GRID ? t : SCM_GRID;
+}
+
+bool smallcin_wgrad_is_mfma(const unet_wgrad_desc* d) { return smallcin_wgrad_mfma_ok(d); }
+
 size_t smallcin_wgrad_ws(const unet_wgrad_desc* d) {
+  if (smallcin_wgrad_mfma_ok(d)) return (size_t)4 * smallcin_wgrad_grid(d, nullptr) * 64 * (2 * 9 * d->Cin) * sizeof(float);
   return (size_t)smallcin_rows((long long)d->N * d->H * d->W) * d->Cout * d->Cin * 9 * sizeof(float);
 }
 
 int smallcin_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
+  if (smallcin_wgrad_mfma_ok(d)) {
+    int t;
+    const int grid = smallcin_wgrad_grid(d, &t);
+    float* part = (float*)d->workspace;
+    if (d->dtype == UNET_BF16)
+      hipLaunchKernelGGL(smallcin_wgrad_mfma_kernel<bf16>, dim3(grid), dim3(256), 0, st, *d, t, part);
+    else
+      hipLaunchKernelGGL(smallcin_wgrad_mfma_kernel<f16>, dim3(grid), dim3(256), 0, st, *d, t, part);
+    int e = check_launch("smallcin_wgrad_mfma");
+    if (e) return e;
+    hipLaunchKernelGGL(smallcin_fold_kernel, dim3(64 * 9 * d->Cin), dim3(256), 0, st, part, 4 * grid, 64, 9 * d->Cin,
+                       d->dw, d->accum);
+    return check_launch("smallcin_fold");
+  }
   const int rows = smallcin_rows((long long)d->N * d->H * d->W);
   float* part = (float*)d->workspace;
   if (d->dtype == UNET_BF16)

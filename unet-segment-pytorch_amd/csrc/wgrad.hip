@@ -224,11 +224,14 @@ static int launch_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
 
 bool wgrad2_eligible(const unet_wgrad_desc* d, size_t* ws_bytes);  // wgrad2.hip
 int wgrad2_run(const unet_wgrad_desc* d, hipStream_t st);
+bool wgrad5_eligible(const unet_wgrad_desc* d, size_t* ws_bytes);  // wgrad5.hip
+int wgrad5_run(const unet_wgrad_desc* d, hipStream_t st);
 bool smallcin_wgrad_ok(const unet_wgrad_desc* d);  // smallcin.hip
 bool pw_wgrad_ok(const unet_wgrad_desc* d);        // pw.hip
 size_t pw_wgrad_ws(const unet_wgrad_desc* d);
 int pw_wgrad(const unet_wgrad_desc* d, hipStream_t st);
 size_t smallcin_wgrad_ws(const unet_wgrad_desc* d);
+bool smallcin_wgrad_is_mfma(const unet_wgrad_desc* d);
 int smallcin_wgrad(const unet_wgrad_desc* d, hipStream_t st);
 
 }  // namespace unet
@@ -249,8 +252,21 @@ size_t unet_wgrad_workspace(const unet_wgrad_desc* d) {
   size_t b = 0;
   if (unet::smallcin_wgrad_ok(d)) return unet::smallcin_wgrad_ws(d);
   if (unet::pw_wgrad_ok(d)) return unet::pw_wgrad_ws(d);
+  if (unet::wgrad5_eligible(d, &b)) return b;
   if (unet::wgrad2_eligible(d, &b)) return b;
   return wg_plan(d).ws_bytes;
+}
+
+int unet_wgrad_variant(const unet_wgrad_desc* d, char* buf, int len) {
+  if (!d || !buf || len <= 0) return UNET_ERR_ARG;
+  const char* tn = d->dtype == UNET_F16 ? "fp16" : d->dtype == UNET_BF16 ? "bf16" : "fp32";
+  if (unet::smallcin_wgrad_ok(d))
+    snprintf(buf, len, unet::smallcin_wgrad_is_mfma(d) ? "smallcin_wgrad_mfma_kernel<%s>" : "smallcin_wgrad_kernel<%s>", tn);
+  else if (unet::pw_wgrad_ok(d)) snprintf(buf, len, "pw_wgrad_kernel<%s>", tn);
+  else if (unet::wgrad5_eligible(d, nullptr)) snprintf(buf, len, "wgrad5_kernel<%s>", tn);
+  else if (unet::wgrad2_eligible(d, nullptr)) snprintf(buf, len, "wgrad2_kernel<%s,%d>", tn, d->ksize);
+  else snprintf(buf, len, "wgrad_kernel<%s,%d>", tn, d->ksize);
+  return 0;
 }
 
 int unet_conv_wgrad(const unet_wgrad_desc* d, void* stream) {
@@ -268,6 +284,7 @@ int unet_conv_wgrad(const unet_wgrad_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (unet::smallcin_wgrad_ok(d)) return unet::smallcin_wgrad(d, st);
   if (unet::pw_wgrad_ok(d)) return unet::pw_wgrad(d, st);
+  if (unet::wgrad5_eligible(d, nullptr)) return unet::wgrad5_run(d, st);
   if (unet::wgrad2_eligible(d, nullptr)) return unet::wgrad2_run(d, st);
   if (d->dtype == UNET_BF16) return d->ksize == 3 ? launch_wgrad<bf16, 3>(d, st) : launch_wgrad<bf16, 1>(d, st);
   if (d->dtype == UNET_F16) return d->ksize == 3 ? launch_wgrad<f16, 3>(d, st) : launch_wgrad<f16, 1>(d, st);

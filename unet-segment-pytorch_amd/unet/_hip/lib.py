@@ -56,6 +56,7 @@ _SIGS = {
     "unet_conv_mtiles": (c_int, [c_int, c_int, c_int]),
     "unet_conv_stats_rows": (c_int, [ctypes.POINTER(ConvDesc)]),
     "unet_conv_variant": (c_int, [ctypes.POINTER(ConvDesc), ctypes.c_char_p, c_int]),
+    "unet_wgrad_variant": (c_int, [ctypes.POINTER(WgradDesc), ctypes.c_char_p, c_int]),
     "unet_pack_weight": (c_int, [c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "unet_packed_weight_elems": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "unet_pack_weights": (c_int, [c_int, c_int, ctypes.POINTER(PackJob), c_vp]),

@@ -102,8 +102,11 @@ def conv_kernel_name(d) -> str:
     return buf.value.decode()
 
 
-def wgrad_kernel_name(prec: "Precision", ksize: int) -> str:
-    return f"wgrad_kernel<{prec.name},{ksize}>"
+def wgrad_kernel_name(wd) -> str:
+    """Weight-gradient kernel unet_conv_wgrad dispatches this descriptor to (csrc/wgrad.hip)."""
+    buf = ctypes.create_string_buffer(128)
+    L.load().unet_wgrad_variant(wd, buf, 128)
+    return buf.value.decode()
 
 
 def require_device(t: torch.Tensor, what: str = "input") -> None:

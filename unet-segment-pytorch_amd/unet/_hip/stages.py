@@ -170,7 +170,7 @@ class ConvBN:
         ws_bytes = L.load().unet_wgrad_workspace(wd)
         ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
         wd.workspace = ws.data_ptr()
-        probe.launch(lambda: wgrad_kernel_name(prec, self.k), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
+        probe.launch(lambda: wgrad_kernel_name(wd), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
                      lambda: L.call("unet_conv_wgrad", wd, stream()))
         grads.put(self.conv.weight, dw)
         if dgrad is None:
@@ -472,7 +472,7 @@ class ConvTStage:
         wd.accum = 0
         ws = torch.empty(max(L.load().unet_wgrad_workspace(wd), 16), dtype=torch.uint8, device=dev)
         wd.workspace = ws.data_ptr()
-        probe.launch(lambda: wgrad_kernel_name(prec, 1), 2.0 * P * self.cin * 4 * ct,
+        probe.launch(lambda: wgrad_kernel_name(wd), 2.0 * P * self.cin * 4 * ct,
                      lambda: L.call("unet_conv_wgrad", wd, stream()))
         grads.put(self.m.weight, dw4.view(2, 2, ct, self.cin).permute(3, 2, 0, 1).contiguous())
         if not need_dx:
