@@ -106,6 +106,10 @@ typedef struct unet_conv_desc {
   const float* bnb_mean;
   const float* bnb_invstd;
   float* bnb_stats;       /* NULL: no reduction                                                    */
+  /* Y mode, optional (unet_conv_act_out_ok): src[0]'s values as the conv reads them (BN-apply, ReLU,
+   * attention gate, layers.py:33-34,192), op dtype [N,H,W,src[0].C], written once — the weight
+   * gradient of this conv then reads a stored map instead of re-applying the transform               */
+  void* act_out;
 } unet_conv_desc;
 
 typedef struct unet_wgrad_desc {
@@ -127,6 +131,8 @@ int unet_conv_mtiles(int N, int H, int W);
 int unet_conv_stats_rows(const unet_conv_desc* d);
 /* name of the kernel instantiation unet_conv dispatches d to (for profiling / roofline probes)   */
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len);
+/* does unet_conv write d->act_out for this descriptor (else the caller keeps the activation source)? */
+int unet_conv_act_out_ok(const unet_conv_desc* d);
 /* name of the weight-gradient kernel unet_conv_wgrad dispatches d to (profiling / tests)          */
 int unet_wgrad_variant(const unet_wgrad_desc* d, char* buf, int len);
 
@@ -257,6 +263,18 @@ int unet_outconv_fwd(int dtype, long long N, int H, int W, int C, int K, const v
 int unet_outconv_bwd(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
                      const float* shift, int relu, const float* w, const float* dlogits_nchw, float* da,
                      int da_accum, float* partial, void* stream);
+/* OutConv backward fused with the BatchNorm backward of its input (the last DoubleConv's output, whose only
+ * consumer is OutConv — unet.py:92, 203; layers.py:120 + 33-37): from y and the logit gradient dl (fp32 NCHW,
+ * n_classes == 2) accumulates OutConv's partials (as unet_outconv_bwd) and the BN-backward sums
+ * bn_partial[2][rows][C] (Σ g_m, Σ g_m·x̂; rows = unet_outconv_rows(P), for unet_bn_bwd_finalize) without storing
+ * the activation gradient g = W^T dl                                                                      */
+int unet_outconv_bwd_bn(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
+                        const float* shift, int relu, const float* w, const float* dl, const float* mean,
+                        const float* invstd, float* partial, float* bn_partial, void* stream);
+/* the matching BN-backward apply: dy = coef0·g_m + coef1·y + coef2 with g recomputed from dl          */
+int unet_bn_bwd_apply_oc(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
+                         const float* shift, int relu, const float* w, const float* dl, const float* coef, void* dy,
+                         void* stream);
 int unet_outconv_bwd_finalize(const float* partial, int rows, int C, int K, float* dw, float* db,
                               int accum, void* stream);
 

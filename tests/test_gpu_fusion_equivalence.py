@@ -15,12 +15,14 @@ pytestmark = pytest.mark.gpu
 def _grads(model, x, t, env, seen=None):
     from unet._hip import lib as L
     from unet.utils.loss import DiceBCELoss
-    old = {k: os.environ.get(k) for k in ("UNET_NO_POOL_FOLD", "UNET_NO_GATE_FUSE")}
+    old = {k: os.environ.get(k) for k in ("UNET_NO_POOL_FOLD", "UNET_NO_GATE_FUSE", "UNET_NO_ACT_OUT", "UNET_NO_OC_FUSE")}
     orig = L.call
 
     def rec(name, *args):
         if seen is not None:
             seen.add(name if name != "unet_conv" else f"unet_conv:{args[0].out_mode}")
+            if name == "unet_conv_wgrad" and args[0].ksize == 3:
+                seen.add(f"wgrad3:src0kind={args[0].src[0].kind}")
         return orig(name, *args)
 
     L.call = rec
@@ -66,3 +68,58 @@ def test_fused_backward_bit_identical(prec, size):
     assert torch.equal(out0, out1)
     diff = [n for n in g0 if not torch.equal(g0[n], g1[n])]
     assert not diff, diff
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_act_out_wgrad_bit_identical(prec):
+    """The forward conv writes its transformed BN-activation input once (unet_conv act_out, conv5) and the
+    3x3 weight gradients read that stored map instead of re-applying BN + ReLU (+ the attention gate): the
+    same 16-bit values in the same MFMA order, so logits and every parameter gradient are bit-identical to
+    the re-transforming path (UNET_NO_ACT_OUT).  2 x 256^2, base 64: the 256^2 / 128^2 convs run on conv5."""
+    from unet.models import AttentionUNet
+    torch.manual_seed(4)
+    m = AttentionUNet(1, 2, base_features=64).cuda().train()
+    m.hip_precision = prec
+    g = torch.Generator().manual_seed(6)
+    x = (torch.rand(2, 1, 256, 256, generator=g) * 2 - 1).cuda()
+    t = (torch.rand(2, 256, 256, generator=g) < 0.1).long().cuda()
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    seen0, seen1 = set(), set()
+    out0, g0 = _grads(m, x, t, {}, seen0)
+    m.load_state_dict(state)
+    out1, g1 = _grads(m, x, t, {"UNET_NO_ACT_OUT": "1"}, seen1)
+    from unet._hip import lib as L
+    plain, act = f"wgrad3:src0kind={L.SRC_PLAIN}", f"wgrad3:src0kind={L.SRC_ACT}"
+    assert plain in seen0 and act in seen1, (sorted(seen0), sorted(seen1))
+    assert torch.equal(out0, out1)
+    diff = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+    assert not diff, diff
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("kind", ["attention", "unet"])
+def test_outconv_bn_backward_fused(prec, kind):
+    """OutConv's backward fused with the BN backward of its input (unet_outconv_bwd_bn + unet_bn_bwd_apply_oc:
+    the activation gradient W^T dl is recomputed, never stored) against the stored-gradient path
+    (UNET_NO_OC_FUSE): the same sums in another order, so equal up to fp32 rounding (fp32 mode), and up to
+    the 16-bit rounding of the dgrad operand that this reorder can flip (bf16 mode)."""
+    from unet.models import AttentionUNet, UNet
+    torch.manual_seed(7)
+    m = (AttentionUNet(1, 2, base_features=16) if kind == "attention" else UNet(1, 2, base_features=16)).cuda().train()
+    m.hip_precision = prec
+    g = torch.Generator().manual_seed(8)
+    x = (torch.rand(2, 1, 96, 128, generator=g) * 2 - 1).cuda()
+    t = (torch.rand(2, 96, 128, generator=g) < 0.1).long().cuda()
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    seen0, seen1 = set(), set()
+    out0, g0 = _grads(m, x, t, {}, seen0)
+    m.load_state_dict(state)
+    out1, g1 = _grads(m, x, t, {"UNET_NO_OC_FUSE": "1"}, seen1)
+    assert "unet_outconv_bwd_bn" in seen0 and "unet_bn_bwd_apply_oc" in seen0
+    assert "unet_outconv_bwd_bn" not in seen1
+    assert torch.equal(out0, out1)
+    tol = 1e-4 if prec == "fp32" else 2e-2
+    for n in g0:
+        a, b = g0[n].double(), g1[n].double()
+        rel = float((a - b).norm() / (b.norm() + 1e-30))
+        assert rel <= tol, (n, rel)

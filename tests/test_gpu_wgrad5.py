@@ -132,3 +132,38 @@ def test_wgrad5_default_policy_at_bench_sizes(monkeypatch):
             wd.src[i] = s
         wd.dy = dy.data_ptr()
         assert R.wgrad_kernel_name(wd).startswith("wgrad5_kernel<bf16"), shape
+
+
+@pytest.mark.parametrize("kind", ["act", "gated+plain"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv5_act_out_matches_transform(prec, kind):
+    """unet_conv act_out (conv5 forward, y mode): the stored map is the transformed src[0] — the weight
+    gradient on [plain(act_out), src1] is bit-identical to the one on the BN-activation sources"""
+    L, R = _lib(), _rt()
+    dt = DT[prec]
+    shape = (4, 256, 256, 128, 64)     # conv5 needs >= 256 output tiles
+    N, H, W, cin, cout = shape
+    srcs, x, dy, keep = _case(shape, kind, dt, seed=8)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * 0.05).to(dt).float()
+    wp = R.pack_weight(w, R._PRECISIONS[prec], transpose=False)
+    d = L.ConvDesc()
+    d.dtype = L.BF16 if dt == torch.bfloat16 else L.F16
+    d.N, d.H, d.W, d.Cin, d.Cout, d.ksize, d.nsrc = N, H, W, cin, cout, 3, len(srcs)
+    for i, s in enumerate(srcs):
+        d.src[i] = s
+    y = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
+    d.weight, d.out_mode, d.out = wp.data_ptr(), L.OUT_Y, y.data_ptr()
+    assert L.load().unet_conv_act_out_ok(d) == 1
+    act = torch.full((N, H, W, srcs[0].C), float("nan"), dtype=dt, device="cuda")
+    d.act_out = act.data_ptr()
+    L.call("unet_conv", d, R.stream())
+    torch.cuda.synchronize()
+    assert not torch.isnan(act.float()).any()          # every pixel written
+    c0 = srcs[0].C
+    assert (act.float() - x[..., :c0]).abs().max() <= 2 ** -7 * (1 + x[..., :c0].abs().max())
+    ps = L.Src()
+    ps.kind, ps.C, ps.H, ps.W, ps.data = L.SRC_PLAIN, c0, H, W, act.data_ptr()
+    a, na = _wgrad(srcs, dy, shape, dt)
+    b, nb = _wgrad([ps] + srcs[1:], dy, shape, dt)
+    assert na == nb, (na, nb)
+    assert torch.equal(a, b)

@@ -21,8 +21,12 @@ wd = L.WgradDesc()
 wd.dtype = L.BF16
 wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = N, H, W, cin, cout, 3, 1
 s = wd.src[0]
-s.kind, s.C, s.H, s.W, s.data = L.SRC_ACT, cin, H, W, y.data_ptr()
-s.scale, s.shift, s.relu = ab[0].data_ptr(), ab[1].data_ptr(), 1
+import os  # noqa: E402
+if os.environ.get("WG_KIND", "act") == "plain":
+    s.kind, s.C, s.H, s.W, s.data = L.SRC_PLAIN, cin, H, W, y.data_ptr()
+else:
+    s.kind, s.C, s.H, s.W, s.data = L.SRC_ACT, cin, H, W, y.data_ptr()
+    s.scale, s.shift, s.relu = ab[0].data_ptr(), ab[1].data_ptr(), 1
 wd.dy = dy.data_ptr()
 dw = torch.empty(cout, cin, 3, 3, device=dev)
 wd.dw = dw.data_ptr()
@@ -37,4 +41,5 @@ ev[1].record()
 torch.cuda.synchronize()
 us = ev[0].elapsed_time(ev[1]) * 1e3 / (reps - reps // 2)
 fl = 2.0 * N * H * W * cin * cout * 9
-print(f"wgrad {N}x{H}x{W} {cin}->{cout}: {us:.1f} us/launch (incl. reduce), {fl / us / 1e6:.1f} TF/s")
+from unet._hip.runtime import wgrad_kernel_name  # noqa: E402
+print(f"{wgrad_kernel_name(wd)} {os.environ.get('WG_KIND', 'act')} {N}x{H}x{W} {cin}->{cout}: {us:.1f} us/launch (incl. reduce), {fl / us / 1e6:.1f} TF/s")

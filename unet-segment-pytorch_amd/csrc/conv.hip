@@ -484,6 +484,7 @@ static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t s
 
 template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
 bool conv5_eligible(const unet_conv_desc* d);   // conv5.hip: the LDS-DMA 3x3 path
+bool conv5_act_out_ok(const unet_conv_desc* d);
 int conv5_run(const unet_conv_desc* d, hipStream_t st);
 int conv5_stats_rows(const unet_conv_desc* d);
 int conv5_variant(const unet_conv_desc* d, char* buf, int len);
@@ -621,6 +622,8 @@ int unet_conv_stats_rows(const unet_conv_desc* d) {
   const ConvCfg c = pick_cfg(d);
   return d->N * cdiv(d->W, CTW) * cdiv(d->H, 4 * c.wm);
 }
+
+int unet_conv_act_out_ok(const unet_conv_desc* d) { return d && conv5_act_out_ok(d) ? 1 : 0; }
 
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
   if (smallcin_conv_ok(d)) {
@@ -760,6 +763,11 @@ int unet_conv(const unet_conv_desc* d, void* stream) {
   }
   if (d->dtype != UNET_BF16 && d->dtype != UNET_F16 && d->dtype != UNET_F32) {
     set_error("unet_conv: bad dtype");
+    return UNET_ERR_ARG;
+  }
+  if (d->act_out && !conv5_act_out_ok(d)) {
+    set_error("unet_conv: act_out is served for y-mode BN-activation sources on the conv5 path only "
+              "(ask unet_conv_act_out_ok)");
     return UNET_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;

@@ -218,6 +218,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
 
   // BN-activation (+gate) transform of the chunk at cursor q, raw -> compute image, this lane's own slots
   // (zero-padding pixels and the image's tail slots come out 0)
+  T* const aout = (ACT && blockIdx.y == 0) ? (T*)d.act_out : nullptr;
   auto transform = [&](const Cur& q) {
     const int cn0 = q.c * 16;
     const bool act = !(d.nsrc > 1 && cn0 >= C0);    // src0 (activation) or src1 (stored: copied)
@@ -250,6 +251,12 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo) * gm;
           q4 = pack8_16<T>(v);
+          // act_out: the first output-channel block writes the transformed interior once (the weight
+          // gradient then reads it as a stored map); a store only adds to the vmcnt waits' conservatism
+          if constexpr (OM == OM5_Y) {
+            if (aout && ok && (unsigned)soy[k] < (unsigned)TH && (unsigned)sox[k] < (unsigned)C5_W)
+              *reinterpret_cast<uint4*>(aout + (((unsigned)q.n * d.H + y) * (unsigned)d.W + x) * (unsigned)C0 + ch) = q4;
+          }
         }
         *reinterpret_cast<uint4*>(cb + s * 16) = q4;
       }
@@ -595,6 +602,12 @@ bool conv5_eligible(const unet_conv_desc* d) {
 }
 
 int conv5_stats_rows(const unet_conv_desc* d) { return conv5_gx(d) * C5_WM; }
+
+// can the forward write src[0]'s transformed input to act_out (the y-mode BN-activation kernel serves d)?
+bool conv5_act_out_ok(const unet_conv_desc* d) {
+  return conv5_eligible(d) && d->out_mode == UNET_OUT_Y && !d->bnb_stats && d->src[0].kind == UNET_SRC_ACT &&
+         d->src[0].C % 16 == 0;
+}
 
 int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
   snprintf(buf, len, "conv5_kernel<%s,%d>", d->dtype == UNET_F16 ? "fp16" : "bf16", C5_MI);

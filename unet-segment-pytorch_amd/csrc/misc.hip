@@ -414,6 +414,135 @@ __global__ __launch_bounds__(256) void outconv_bwd_vec_kernel(long long P, int H
   }
 }
 
+// OutConv backward fused with the BatchNorm backward of its input activation (the last DoubleConv's output,
+// whose only consumer is OutConv: unet.py:92 / :203).  The activation gradient g[px][c] = Σ_k W[k][c]·dl[k][px]
+// is never stored: this pass accumulates OutConv's dW / db partials (as outconv_bwd_vec_kernel) and the
+// BatchNorm-backward sums Σ g_m, Σ g_m·x̂ (g_m: g where the ReLU passed, as bn_bwd_reduce_vec_kernel) from
+// one read of y and the 2-class logit gradient; bn_bwd_apply_oc_kernel recomputes g the same way.  Removes the
+// fp32 [N,H,W,C] gradient write and its two reads (3 x 268 MB at 4 x 512^2 x 64).
+template <typename T, int KK>
+__global__ __launch_bounds__(256) void outconv_bwd_bn_kernel(long long P, int HW, int C, int G, const T* y,
+                                                             const float* sc, const float* sf, int relu,
+                                                             const float* w, const float* dl, const float* mean,
+                                                             const float* invstd, float* part, float* bpart, int rows) {
+  constexpr int F = KK * 8 + KK;  // per-thread partials: dw[k][8], db[k]
+  __shared__ float sh[256 * F];
+  const int tid = threadIdx.x, v = tid % G, py = tid / G, R = 256 / G;
+  const int c0 = v * 8;
+  float s8[8], f8[8], mu[8], is[8], wk[KK][8], dw[KK][8], db[KK], sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s8[j] = sc[c0 + j];
+    f8[j] = sf[c0 + j];
+    mu[j] = mean[c0 + j];
+    is[j] = invstd[c0 + j];
+    sg[j] = 0.f;
+    sgx[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KK; ++k) { wk[k][j] = w[k * C + c0 + j]; dw[k][j] = 0.f; }
+  }
+#pragma unroll
+  for (int k = 0; k < KK; ++k) db[k] = 0.f;
+  const float lo = relu ? 0.f : -INFINITY;
+  const long long per = (P + gridDim.x - 1) / gridDim.x;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  for (long long q = p0 + py; q < p1; q += R) {
+    const long long n = q / HW, hw = q % HW;
+    float dlk[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) { dlk[k] = dl[(n * KK + k) * HW + hw]; db[k] += dlk[k]; }
+    float yv[8];
+    load_vec<T>(y + q * C + c0, yv);
+    if constexpr (sizeof(T) == 4) load_vec<T>(y + q * C + c0 + 4, yv + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float pre = yv[j] * s8[j] + f8[j];
+      const float a = fmaxf(pre, lo);
+      float g = 0.f;
+#pragma unroll
+      for (int k = 0; k < KK; ++k) { g += wk[k][j] * dlk[k]; dw[k][j] += dlk[k] * a; }
+      const float gm = (relu && !(pre > 0.f)) ? 0.f : g;
+      sg[j] += gm;
+      sgx[j] += gm * (yv[j] - mu[j]) * is[j];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sh[tid * F + k * 8 + j] = dw[k][j];
+    sh[tid * F + KK * 8 + k] = db[k];
+  }
+  __syncthreads();
+  for (int e = tid; e < C * KK + KK; e += 256) {
+    float acc = 0.f;
+    if (e < C * KK) {
+      const int k = e / C, c = e % C, vv = c / 8, j = c % 8;
+      for (int r = 0; r < R; ++r) acc += sh[(r * G + vv) * F + k * 8 + j];
+      part[((size_t)blockIdx.x * (KK + 1) + k) * C + c] = acc;
+    } else {
+      const int k = e - C * KK;
+      for (int r = 0; r < R; ++r) acc += sh[(r * G) * F + KK * 8 + k];
+      part[((size_t)blockIdx.x * (KK + 1) + KK) * C + k] = acc;
+    }
+  }
+  __syncthreads();
+  // BatchNorm-backward partial sums of the block: [2][rows][C] (unet_bn_bwd_finalize's layout)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[tid] = sg[j];
+    sh[256 + tid] = sgx[j];
+    __syncthreads();
+    if (tid < G) {
+      float a = 0.f, b = 0.f;
+      for (int r = 0; r < R; ++r) { a += sh[r * G + tid]; b += sh[256 + r * G + tid]; }
+      bpart[(size_t)blockIdx.x * C + tid * 8 + j] = a;
+      bpart[((size_t)rows + blockIdx.x) * C + tid * 8 + j] = b;
+    }
+    __syncthreads();
+  }
+}
+
+// dy = A·g_m + B·y + C with g recomputed from the logit gradient (bn_bwd_apply_vec_kernel's formula)
+template <typename T, int KK>
+__global__ __launch_bounds__(256) void bn_bwd_apply_oc_kernel(long long P, int HW, int C, const T* y, const float* scale,
+                                                              const float* shift, int relu, const float* w,
+                                                              const float* dl, const float* coef, T* dy) {
+  const int CV = C / 8;
+  const long long total = P * CV;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const int cv = (int)(e % CV);  // fixed: the stride is a multiple of CV (power of two <= 256)
+  float sc[8], sf[8], A[8], B[8], Cc[8], wk[KK][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cv * 8 + j;
+    sc[j] = scale[c]; sf[j] = shift[c]; A[j] = coef[c]; B[j] = coef[C + c]; Cc[j] = coef[2 * C + c];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) wk[k][j] = w[k * C + c];
+  }
+  const int cvs = __builtin_ctz(CV);
+  for (; e < total; e += stride) {
+    const long long p = e >> cvs;
+    const unsigned n = (unsigned)p / (unsigned)HW, hw = (unsigned)p - n * (unsigned)HW;
+    float dlk[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) dlk[k] = dl[((size_t)n * KK + k) * HW + hw];
+    float yv[8], o[8];
+    load_vec<T>(y + p * C + cv * 8, yv);
+    if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float g = 0.f;
+#pragma unroll
+      for (int k = 0; k < KK; ++k) g += wk[k][j] * dlk[k];
+      const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g;
+      o[j] = A[j] * gj + B[j] * yv[j] + Cc[j];
+    }
+    store_vec<T>(dy + p * C + cv * 8, o);
+    if constexpr (sizeof(T) == 4) store_vec<T>(dy + p * C + cv * 8 + 4, o + 4);
+  }
+}
+
 // one block per output element; fixed-order fp64 block reduction over the partial rows
 __global__ void outconv_bwd_finalize_kernel(const float* part, int rows, int C, int K, float* dw, float* db, int accum) {
   __shared__ double sh[4];
@@ -772,6 +901,53 @@ int unet_outconv_bwd(int dtype, long long N, int H, int W, int C, int K, const v
     hipLaunchKernelGGL(outconv_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, P, H * W, C, cl, K,
                        (const float*)y, scale, shift, relu, w, dl, da, accum, partial, rows);
   return check_launch("outconv_bwd");
+}
+
+int unet_outconv_bwd_bn(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
+                        const float* shift, int relu, const float* w, const float* dl, const float* mean,
+                        const float* invstd, float* partial, float* bn_partial, void* stream) {
+  const long long P = N * H * (long long)W;
+  const int G = C / 8;
+  if (K != 2 || C % 8 || G > 256 || (G & (G - 1)) || !scale || !shift || !mean || !invstd || P >= (1LL << 31)) {
+    set_error("unet_outconv_bwd_bn: needs n_classes == 2, C % 8 == 0, C/8 a power of two <= 256, a BN activation");
+    return UNET_ERR_UNSUPPORTED;
+  }
+  const int rows = oc_rows(P);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL((outconv_bwd_bn_kernel<f16, 2>), dim3(rows), dim3(256), 0, st, P, H * W, C, G, (const f16*)y,
+                       scale, shift, relu, w, dl, mean, invstd, partial, bn_partial, rows);
+  else if (dtype == UNET_BF16)
+    hipLaunchKernelGGL((outconv_bwd_bn_kernel<bf16, 2>), dim3(rows), dim3(256), 0, st, P, H * W, C, G, (const bf16*)y,
+                       scale, shift, relu, w, dl, mean, invstd, partial, bn_partial, rows);
+  else
+    hipLaunchKernelGGL((outconv_bwd_bn_kernel<float, 2>), dim3(rows), dim3(256), 0, st, P, H * W, C, G,
+                       (const float*)y, scale, shift, relu, w, dl, mean, invstd, partial, bn_partial, rows);
+  return check_launch("outconv_bwd_bn");
+}
+
+int unet_bn_bwd_apply_oc(int dtype, long long N, int H, int W, int C, int K, const void* y, const float* scale,
+                         const float* shift, int relu, const float* w, const float* dl, const float* coef, void* dy,
+                         void* stream) {
+  const long long P = N * H * (long long)W;
+  const int CV = C / 8;
+  if (K != 2 || C % 8 || CV > 256 || (CV & (CV - 1)) || P >= (1LL << 31)) {
+    set_error("unet_bn_bwd_apply_oc: needs n_classes == 2, C % 8 == 0, C/8 a power of two <= 256");
+    return UNET_ERR_UNSUPPORTED;
+  }
+  long long b = (P * CV + 255) / 256;
+  if (b > 8192) b = 8192;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == UNET_F16)
+    hipLaunchKernelGGL((bn_bwd_apply_oc_kernel<f16, 2>), dim3((int)b), dim3(256), 0, st, P, H * W, C, (const f16*)y,
+                       scale, shift, relu, w, dl, coef, (f16*)dy);
+  else if (dtype == UNET_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_oc_kernel<bf16, 2>), dim3((int)b), dim3(256), 0, st, P, H * W, C, (const bf16*)y,
+                       scale, shift, relu, w, dl, coef, (bf16*)dy);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_oc_kernel<float, 2>), dim3((int)b), dim3(256), 0, st, P, H * W, C,
+                       (const float*)y, scale, shift, relu, w, dl, coef, (float*)dy);
+  return check_launch("bn_bwd_apply_oc");
 }
 
 int unet_outconv_bwd_finalize(const float* partial, int rows, int C, int K, float* dw, float* db, int accum,

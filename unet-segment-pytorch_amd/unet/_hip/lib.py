@@ -33,7 +33,7 @@ class ConvDesc(ctypes.Structure):
                 ("out", c_vp), ("out2", c_vp), ("split", c_int), ("accum", c_int), ("accum2", c_int),
                 ("stats", c_vp), ("pool_src", Src), ("bias", c_vp), ("pool_code", c_vp),
                 ("bnb_y", c_vp), ("bnb_scale", c_vp), ("bnb_shift", c_vp), ("bnb_relu", c_int), ("bnb_mean", c_vp),
-                ("bnb_invstd", c_vp), ("bnb_stats", c_vp)]
+                ("bnb_invstd", c_vp), ("bnb_stats", c_vp), ("act_out", c_vp)]
 
 
 class PackJob(ctypes.Structure):
@@ -57,6 +57,7 @@ _SIGS = {
     "unet_conv_stats_rows": (c_int, [ctypes.POINTER(ConvDesc)]),
     "unet_conv_variant": (c_int, [ctypes.POINTER(ConvDesc), ctypes.c_char_p, c_int]),
     "unet_wgrad_variant": (c_int, [ctypes.POINTER(WgradDesc), ctypes.c_char_p, c_int]),
+    "unet_conv_act_out_ok": (c_int, [ctypes.POINTER(ConvDesc)]),
     "unet_pack_weight": (c_int, [c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "unet_packed_weight_elems": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "unet_pack_weights": (c_int, [c_int, c_int, ctypes.POINTER(PackJob), c_vp]),
@@ -98,6 +99,10 @@ _SIGS = {
                                  c_vp]),
     "unet_outconv_bwd": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
                                  c_int, c_vp, c_vp]),
+    "unet_outconv_bwd_bn": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
+                                    c_vp, c_vp, c_vp, c_vp]),
+    "unet_bn_bwd_apply_oc": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
+                                     c_vp, c_vp]),
     "unet_outconv_bwd_finalize": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "unet_nchw_to_nhwc": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "unet_nhwc_to_nchw": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),

@@ -188,7 +188,7 @@ class Act:
     for a single-consumer activation in bf16 mode (`grad_single`)."""
 
     __slots__ = ("data", "N", "H", "W", "C", "ab", "relu", "mean", "invstd", "grad", "_grad_init", "keep",
-                 "bn_owned", "pool_grad", "batch_stats")
+                 "bn_owned", "pool_grad", "batch_stats", "oc_fused")
 
     def __init__(self, data: torch.Tensor, ab: Optional[torch.Tensor], relu: bool,
                  mean: Optional[torch.Tensor] = None, invstd: Optional[torch.Tensor] = None):
@@ -206,6 +206,9 @@ class Act:
         self.bn_owned = False
         self.pool_grad = None
         self.batch_stats = True   # False: an eval-mode BN (running statistics) produced it
+        # set by OutConvStage.backward when OutConv is the only consumer: (dl, w, K, bn partial sums, rows) — the
+        # gradient W^T dl is recomputed by the BN-backward apply instead of being stored
+        self.oc_fused = None
 
     @property
     def scale(self):

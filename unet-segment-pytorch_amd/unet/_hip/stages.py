@@ -69,6 +69,8 @@ class ConvBN:
         self.cin, self.cout = conv.in_channels, conv.out_channels
         self.pre_wp = None   # packed forward / dgrad weights, set by NetworkPlan's batched pack
         self.pre_wt = None
+        self.wsrcs = None    # weight-gradient sources when the forward stored its transformed input
+        self.wact = None
 
     # ---- forward ----
     def forward(self, prec: Precision, srcs: List[L.Src], N: int, H: int, W: int, training: bool,
@@ -80,6 +82,15 @@ class ConvBN:
         d = _conv_desc(prec, N, H, W, self.cin, self.cout, self.k, srcs, wp)
         d.out_mode = L.OUT_Y
         d.out = y.data_ptr()
+        # the weight gradient's input: src[0] is a BN activation (+gate) that this forward transforms anyway;
+        # where the kernel can write it once (act_out), the wgrad reads that stored map instead
+        self.wsrcs = self.wact = None
+        if training and srcs[0].kind == L.SRC_ACT and not os.environ.get("UNET_NO_ACT_OUT") \
+                and L.load().unet_conv_act_out_ok(d):
+            act = torch.empty(N, H, W, srcs[0].C, dtype=prec.torch_dtype, device=dev)
+            d.act_out = act.data_ptr()
+            self.wsrcs = [_plain_src(act)] + list(srcs[1:])
+            self.wact = act              # the descriptors hold raw pointers: keep the tensor alive
         bn = self.bn
         ab = f32(2, self.cout, device=dev)
         use_batch = training or not bn.track_running_stats
@@ -116,6 +127,8 @@ class ConvBN:
         dev = a.data.device
         P, C = a.pixels, a.C
         pool = a.pool_grad
+        if a.oc_fused is not None:
+            return self._bn_backward_oc(prec, a, grads)
         assert a.has_grad() or pool is not None, "activation gradient missing"
         gcode = {torch.bfloat16: L.BF16, torch.float16: L.F16}.get(a.grad.dtype, L.F32) if a.has_grad() else L.F32
         if pool is not None:
@@ -150,6 +163,23 @@ class ConvBN:
                    int(a.relu), vp(coef), vp(dy), stream())
         return dy
 
+    def _bn_backward_oc(self, prec: Precision, a: Act, grads: Grads) -> torch.Tensor:
+        """BatchNorm2d(+ReLU) backward of OutConv's input: the sums came from unet_outconv_bwd_bn, the apply
+        recomputes OutConv's input gradient from the logit gradient (unet_bn_bwd_apply_oc)."""
+        dl, w, k, part, rows = a.oc_fused
+        a.oc_fused = None
+        dev = a.data.device
+        C = a.C
+        dgamma, dbeta, coef = f32(C, device=dev), f32(C, device=dev), f32(3, C, device=dev)
+        L.call("unet_bn_bwd_finalize", vp(part[0]), vp(part[1]), rows, C, a.pixels if a.batch_stats else 0,
+               vp(self.bn.weight), vp(a.mean), vp(a.invstd), vp(dgamma), vp(dbeta), 0, vp(coef), stream())
+        grads.put(self.bn.weight, dgamma)
+        grads.put(self.bn.bias, dbeta)
+        dy = torch.empty(a.N, a.H, a.W, C, dtype=prec.torch_dtype, device=dev)
+        L.call("unet_bn_bwd_apply_oc", prec.code, a.N, a.H, a.W, C, k, vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+               int(a.relu), vp(w), vp(dl), vp(coef), vp(dy), stream())
+        return dy
+
     def conv_backward(self, prec: Precision, dy: torch.Tensor, srcs: List[L.Src], grads: Grads,
                       dgrad: Optional[dict]):
         """wgrad into grads[conv.weight]; dgrad routed by `dgrad`:
@@ -160,6 +190,8 @@ class ConvBN:
         wd = L.WgradDesc()
         wd.dtype = prec.code
         wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize = N, H, W, self.cin, self.cout, self.k
+        if self.wsrcs is not None:
+            srcs = self.wsrcs          # the forward's stored copy of its (transformed) input
         wd.nsrc = len(srcs)
         for i, s in enumerate(srcs):
             wd.src[i] = s
@@ -173,6 +205,7 @@ class ConvBN:
         probe.launch(lambda: wgrad_kernel_name(wd), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
                      lambda: L.call("unet_conv_wgrad", wd, stream()))
         grads.put(self.conv.weight, dw)
+        self.wsrcs = self.wact = None
         if dgrad is None:
             return
         wt = self.pre_wt if self.pre_wt is not None else pack_weight(self.conv.weight, prec, transpose=True)
@@ -601,9 +634,11 @@ class DownStage:
 class OutConvStage:
     """OutConv: 1x1 conv with bias -> fp32 NCHW logits — layers.py:109-123."""
 
-    def __init__(self, m):
+    def __init__(self, m, sole_consumer: bool = False):
         self.conv = m.conv
         self.k = self.conv.out_channels
+        # True for the network's OutConv: the last decoder activation feeds nothing else (unet.py:92, 203)
+        self.sole_consumer = sole_consumer
 
     def forward(self, prec, a: Act) -> torch.Tensor:
         self.a = a
@@ -621,9 +656,21 @@ class OutConvStage:
         dl = dlogits.float().contiguous()
         rows = L.load().unet_outconv_rows(a.pixels)
         part = f32(rows, self.k + 1, max(a.C, self.k), device=dev)
-        g, acc = a.grad_target()
-        L.call("unet_outconv_bwd", prec.code, a.N, a.H, a.W, a.C, self.k, vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
-               int(a.relu), vp(self.w), vp(dl), vp(g), acc, vp(part), stream())
+        cv = a.C // 8
+        if (self.sole_consumer and a.bn_owned and not a.has_grad() and a.pool_grad is None and self.k == 2
+                and a.C % 8 == 0 and cv <= 256 and cv & (cv - 1) == 0 and a.pixels < 2 ** 31
+                and not os.environ.get("UNET_NO_OC_FUSE")):
+            # OutConv is the activation's only consumer: its gradient W^T dl is not stored; the BN-backward sums
+            # are taken here and the BN apply recomputes it (unet_outconv_bwd_bn / unet_bn_bwd_apply_oc)
+            bpart = f32(2, rows, a.C, device=dev)
+            L.call("unet_outconv_bwd_bn", prec.code, a.N, a.H, a.W, a.C, self.k, vp(a.data), vp(a.ab[0]),
+                   vp(a.ab[1]), int(a.relu), vp(self.w), vp(dl), vp(a.mean), vp(a.invstd), vp(part), vp(bpart),
+                   stream())
+            a.oc_fused = (dl, self.w, self.k, bpart, rows)
+        else:
+            g, acc = a.grad_target()
+            L.call("unet_outconv_bwd", prec.code, a.N, a.H, a.W, a.C, self.k, vp(a.data), vp(a.ab[0]), vp(a.ab[1]),
+                   int(a.relu), vp(self.w), vp(dl), vp(g), acc, vp(part), stream())
         dw, db = f32(self.k, a.C, 1, 1, device=dev), f32(self.k, device=dev)
         L.call("unet_outconv_bwd_finalize", vp(part), rows, a.C, self.k, vp(dw), vp(db), 0, stream())
         grads.put(self.conv.weight, dw)
@@ -675,7 +722,7 @@ class NetworkPlan:
         self.inc = DoubleConvStage(model.inc)
         self.downs = [DownStage(getattr(model, f"down{i}")) for i in range(1, 5)]
         self.ups = [UpStage(getattr(model, f"up{i}"), attention) for i in range(1, 5)]
-        self.outc = OutConvStage(model.outc)
+        self.outc = OutConvStage(model.outc, sole_consumer=True)
         self.ds = attention and getattr(model, "deep_supervision", False)
         if self.ds:
             self.heads = [DSHeadStage(model.ds_out1), DSHeadStage(model.ds_out2), DSHeadStage(model.ds_out3)]
