@@ -267,7 +267,7 @@ def test_c5_fp16_1024_vs_oracle(c5_ref):
     log = []
     m, out, loss, grads = hip_run(ref["init"], ref["x"], ref["t"], "fp16", in_ch=3, log=log)
     names = _assert_16bit_paths(log, "fp16")
-    assert "smallcin_fwd_kernel<fp16>" in names, sorted(names)
+    assert "smallcin_fwd_mfma_kernel<fp16>" in names, sorted(names)
     print()
     e, agree, lrel, r = report16("C5 fp16 HIP     ", out, loss, grads, f64)
     e_a, agree_a, _, r_a = report16("C5 fp16 autocast", ac["out"], ac["loss"], ac["grads"], f64)

@@ -120,25 +120,29 @@ def test_wgrad5_deterministic(shape, monkeypatch):
 
 
 def test_wgrad5_default_policy_at_bench_sizes(monkeypatch):
-    """the default dispatch (UNET_WGRAD5 unset) sends the bench's 512^2 and 256^2 3x3 weight gradients to wgrad5"""
+    """the default dispatch (UNET_WGRAD5 unset) at the bench's sizes: stored sources (the forward's act_out,
+    materialised pool / upsample) and >= 128 output channels go to wgrad5; a BN-activation source feeding a
+    64-channel output stays on wgrad2 (measured faster there)"""
     monkeypatch.delenv("UNET_WGRAD5", raising=False)
-    for shape in [(4, 512, 512, 64, 64), (4, 256, 256, 128, 128), (4, 512, 512, 128, 64)]:
-        srcs, x, dy, keep = _case(shape, "act" if shape[3] == 64 else "gated+plain", torch.bfloat16)
-        L, R = _lib(), _rt()
+    L, R = _lib(), _rt()
+    for shape, kind, want in [((4, 512, 512, 64, 64), "plain", "wgrad5"), ((4, 512, 512, 128, 64), "plain", "wgrad5"),
+                              ((4, 256, 256, 128, 128), "gated+plain", "wgrad5"),
+                              ((4, 512, 512, 64, 64), "act", "wgrad2"), ((4, 512, 512, 128, 64), "gated+plain", "wgrad2")]:
+        srcs, x, dy, keep = _case(shape, kind, torch.bfloat16)
         N, H, W, cin, cout = shape
         wd = L.WgradDesc()
         wd.dtype, wd.N, wd.H, wd.W, wd.Cin, wd.Cout, wd.ksize, wd.nsrc = L.BF16, N, H, W, cin, cout, 3, len(srcs)
         for i, s in enumerate(srcs):
             wd.src[i] = s
         wd.dy = dy.data_ptr()
-        assert R.wgrad_kernel_name(wd).startswith("wgrad5_kernel<bf16"), shape
+        assert R.wgrad_kernel_name(wd).startswith(f"{want}_kernel<bf16"), (shape, kind)
 
 
 @pytest.mark.parametrize("kind", ["act", "gated+plain"])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 def test_conv5_act_out_matches_transform(prec, kind):
     """unet_conv act_out (conv5 forward, y mode): the stored map is the transformed src[0] — the weight
-    gradient on [plain(act_out), src1] is bit-identical to the one on the BN-activation sources"""
+    gradient on [plain(act_out), src1] equals the one on the BN-activation sources up to fp32 summation order"""
     L, R = _lib(), _rt()
     dt = DT[prec]
     shape = (4, 256, 256, 128, 64)     # conv5 needs >= 256 output tiles
@@ -165,5 +169,8 @@ def test_conv5_act_out_matches_transform(prec, kind):
     ps.kind, ps.C, ps.H, ps.W, ps.data = L.SRC_PLAIN, c0, H, W, act.data_ptr()
     a, na = _wgrad(srcs, dy, shape, dt)
     b, nb = _wgrad([ps] + srcs[1:], dy, shape, dt)
-    assert na == nb, (na, nb)
-    assert torch.equal(a, b)
+    # the same 16-bit operands; the dispatcher may pick another kernel for the stored source (wgrad5 with 4-row
+    # stages for a 64-channel output block vs wgrad2 for the BN-activation source): the same fp32 products
+    # summed in another order
+    rel = float((a - b).double().norm() / b.double().norm())
+    assert rel <= 1e-5, rel

@@ -19,8 +19,9 @@ fams = dict(a.split("=", 1) for a in sys.argv[4:])
 def per_dispatch(d, cname, sub):
     rows = list(csv.DictReader(open(glob.glob(d + "/**/*counter_collection.csv", recursive=True)[0])))
     tot, ids = 0.0, set()
+    alts = sub.split("|")     # 'a|b': kernels whose name contains any alternative (the bench's conv family)
     for r in rows:
-        if sub in r["Kernel_Name"] and r["Counter_Name"] == cname:
+        if any(a in r["Kernel_Name"] for a in alts) and r["Counter_Name"] == cname:
             tot += float(r["Counter_Value"])
             ids.add(r["Dispatch_Id"])
     return tot / max(1, len(ids)) * 1024.0, len(ids)

@@ -59,7 +59,8 @@ struct C5Layout {
   static constexpr int OFF_GATE = OFF_W + 3 * WIMG;
   static constexpr int GATE = NI * 256;             // per-lane gate pre-activations of one tile
   static constexpr int OFF_TAB = OFF_GATE + (ACT ? 2 * GATE : 0);
-  static constexpr int OFF_JUNK = OFF_TAB + (ACT ? 2 * C5_CMAX * 4 : 0);   // target of the filler DMAs
+  static constexpr int OFF_BTAB = OFF_TAB + (ACT ? 2 * C5_CMAX * 4 : 0);   // BNB: the block's BN affine
+  static constexpr int OFF_JUNK = OFF_BTAB + 2 * C5_BN * 4;                   // target of the filler DMAs
   static constexpr int BYTES = OFF_JUNK + 1024;
 };
 
@@ -218,7 +219,9 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
 
   // BN-activation (+gate) transform of the chunk at cursor q, raw -> compute image, this lane's own slots
   // (zero-padding pixels and the image's tail slots come out 0)
-  T* const aout = (ACT && blockIdx.y == 0) ? (T*)d.act_out : nullptr;
+  T* const aout = (ACT && OM == OM5_Y && blockIdx.y == 0) ? (T*)d.act_out : nullptr;
+  const rsrc_t rao = mk_rsrc(aout ? (const void*)aout : d.out, (unsigned)(npix * C0 * 2));
+  bool ns_prev = false;   // the last transform issued DPW act_out stores (after the DMA batch the next wait needs)
   auto transform = [&](const Cur& q) {
     const int cn0 = q.c * 16;
     const bool act = !(d.nsrc > 1 && cn0 >= C0);    // src0 (activation) or src1 (stored: copied)
@@ -252,15 +255,27 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
           for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo) * gm;
           q4 = pack8_16<T>(v);
           // act_out: the first output-channel block writes the transformed interior once (the weight
-          // gradient then reads it as a stored map); a store only adds to the vmcnt waits' conservatism
+          // gradient then reads it as a stored map) — a buffer store per slot, out-of-range for halo and
+          // padding slots, so every transform of an activation chunk issues exactly DPW (ns_prev: the next
+          // chunk's wait leaves them in flight)
           if constexpr (OM == OM5_Y) {
-            if (aout && ok && (unsigned)soy[k] < (unsigned)TH && (unsigned)sox[k] < (unsigned)C5_W)
-              *reinterpret_cast<uint4*>(aout + (((unsigned)q.n * d.H + y) * (unsigned)d.W + x) * (unsigned)C0 + ch) = q4;
+            if (aout) {
+              const bool in = ok && (unsigned)soy[k] < (unsigned)TH && (unsigned)sox[k] < (unsigned)C5_W;
+              const unsigned vo = in ? ((((unsigned)q.n * d.H + y) * (unsigned)d.W + x) * (unsigned)C0 + ch) * 2u : OOB;
+              typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q4), rao, (int)vo, 0, 0);
+            }
           }
         }
         *reinterpret_cast<uint4*>(cb + s * 16) = q4;
+      } else if constexpr (OM == OM5_Y) {
+        if (aout && act) {
+          typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rao, (int)OOB, 0, 0);
+        }
       }
     }
+    if constexpr (OM == OM5_Y) ns_prev = aout && act;
   };
 
   // ---- prologue: scale/shift table, chunks 0-2 in flight, chunk 0 ready ----
@@ -268,6 +283,16 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     float* tab = reinterpret_cast<float*>(lds + Lay::OFF_TAB);
     for (int c = tid; c < C0; c += C5_NT) { tab[c] = s0.scale[c]; tab[C5_CMAX + c] = s0.shift[c]; }
     if (tid < 8) { tab[C0 + tid] = 0.f; tab[C5_CMAX + C0 + tid] = 0.f; }
+  }
+  if constexpr (OM == OM5_BNB) {
+    // the BN affine of the activation whose gradient this dgrad writes (its ReLU mask), the block's channels
+    float* bt = reinterpret_cast<float*>(lds + Lay::OFF_BTAB);
+    if (tid < C5_BN) {
+      const int co = (int)blockIdx.y * C5_BN + tid;
+      const bool ok = co < d.Cout && d.bnb_relu;
+      bt[tid] = ok ? d.bnb_scale[co] : 0.f;
+      bt[C5_BN + tid] = ok ? d.bnb_shift[co] : 0.f;
+    }
   }
   // cursors: I = the next chunk to DMA, X = the next chunk to transform (ACT), K = the chunk being computed.
   // G >= 2 (nch >= 2).  The youngest DMA'd chunk's instruction count decides each wait: ND, ND + DPW (gate
@@ -317,18 +342,37 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   };
   // this wave's DMAs of the chunk after K have landed: only the youngest chunk's may still be in flight
   // (the y epilogue's NST stores sit between DMA batches for the two chunks after it: sw counts them down)
-  constexpr int NST = OM == OM5_Y ? 2 * MI : 0;
+  // (BNB: the epilogue's 4 MI 8-byte g stores likewise; and the tile's NYL y1 loads, issued at the start of
+  // its last chunk — after the two in-flight DMA batches — are counted by that chunk's wait: yl)
+  constexpr int NST = OM == OM5_Y ? 2 * MI : (OM == OM5_BNB || OM == OM5_F32 ? 4 * MI : 0);
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  // F32 without accumulation: counted buffer stores (no RMW loads, whose compiler waits drain the DMA queue)
+  const bool f32_counted = OM == OM5_F32 && !d.accum && !d.accum2 && (d.split % 8) == 0 &&
+                           (double)npix * d.Cout * 4 < (double)OOB;
+  const rsrc_t rf1 = mk_rsrc(d.out, (unsigned)(f32_counted ? npix * d.split * 4 : 0));
+  const rsrc_t rf2 = mk_rsrc(d.out2 ? d.out2 : d.out, (unsigned)(f32_counted ? npix * (d.Cout - d.split) * 4 : 0));
+  constexpr int NYL = OM == OM5_BNB ? 4 * MI : 0;
   int sw = 0;
-  auto wait_next = [&]() {
+  auto wait_next = [&](bool yl) {
+    const bool st = NST && sw > 0;
     if (!y_live) wait_vm<0>();
-    else if (NST && sw > 0) {
+    else if (NYL && yl) {
+      if (y_big) wait_vm<ND + DPW + NYL>();
+      else wait_vm<ND + NYL>();
+    } else if (st && ns_prev) {
+      if (y_big) wait_vm<ND + DPW + NST + DPW>();
+      else wait_vm<ND + NST + DPW>();
+    } else if (st) {
       if (y_big) wait_vm<ND + DPW + NST>();
       else wait_vm<ND + NST>();
+    } else if (ns_prev) {
+      if (y_big) wait_vm<ND + DPW + DPW>();
+      else wait_vm<ND + DPW>();
     } else {
       if (y_big) wait_vm<ND + DPW>();
       else wait_vm<ND>();
     }
-    if (NST && sw > 0) --sw;
+    if (st) --sw;
   };
   auto issue_next = [&]() {
     // called right after a chunk's barrier: every wave has finished reading chunk K, whose ring slots
@@ -341,6 +385,26 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   };
 
   F xA[MI + 2], wA[3], xB[MI + 2], wB[3];
+  // BNB: the activation y1 of this wave's tile pixels (buffer loads, out-of-range offsets for masked lanes:
+  // a fixed count), loaded during the tile's last chunk so that the epilogue's wait for them does not drain
+  // the next chunks' DMAs (their issue follows the epilogue)
+  uint2 yv[OM == OM5_BNB ? MI : 1][4];
+  const rsrc_t ry1 = mk_rsrc(OM == OM5_BNB ? d.bnb_y : d.out, (unsigned)(npix * d.Cout * 2));
+  auto load_y1 = [&](int ti) {
+    int n, h0, w0;
+    tile_of(ti, n, h0, w0);
+    const int ow = w0 + (lane & 31), oh0 = h0 + wm * MI;
+    const unsigned pix0 = ((unsigned)n * d.H + oh0) * (unsigned)d.W + ow;
+#pragma unroll
+    for (int i = 0; i < (OM == OM5_BNB ? MI : 0); ++i)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int co = cw0 + 8 * gq + 4 * (lane >> 5);
+        const bool ok = ow < d.W && oh0 + i < d.H && co < d.Cout;
+        const unsigned vo = ok ? ((pix0 + (unsigned)i * d.W) * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
+        yv[i][gq] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ry1, (int)vo, 0, 0));
+      }
+  };
   for (int ti = 0; ti < ntl; ++ti) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -350,11 +414,15 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     for (int c = 0; c < nch; ++c) {
       // one tap column at a time; the barrier ends the chunk (after it: chunk K's slots are free and the
       // next chunk is readable by every wave)
+      const bool last = c == nch - 1;
+      if constexpr (OM == OM5_BNB) {
+        if (last) load_y1(ti);
+      }
       load_col(K, 0, xA, wA);
       mma_col(xA, wA);
       load_col(K, 1, xB, wB);
       mma_col(xB, wB);
-      wait_next();
+      wait_next(last);
       if constexpr (ACT && !(ABL & 16)) {
         if (X.ti < ntl) {
           transform(X);
@@ -364,7 +432,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       load_col(K, 2, xA, wA);
       mma_col(xA, wA);
       if constexpr (!(ABL & 8)) lds_barrier();
-      issue_next();
+      if (OM != OM5_BNB || !last) issue_next();
       cur_next(K);
     }
 
@@ -424,37 +492,29 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
           }
       }
     } else if constexpr (OM == OM5_BNB) {
-      T* y = (T*)d.out;
-      const T* y1 = (const T*)d.bnb_y;
-      uint2 yv[MI][4];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int co = cw0 + 8 * gq + 4 * hh;
-          yv[i][gq] = make_uint2(0u, 0u);
-          if (colok && i < rows && co < d.Cout)
-            yv[i][gq] = *reinterpret_cast<const uint2*>(y1 + (size_t)(pix0 + (unsigned)i * d.W) * d.Cout + co);
-        }
+      // g stored as buffer stores (fixed count NST, out-of-range offsets mask lanes); the BN affine of the
+      // block's channels from the LDS table the prologue filled; y1 from the loads of the last chunk
+      const float* btab = reinterpret_cast<const float*>(lds + Lay::OFF_BTAB);
+      const rsrc_t rg = mk_rsrc(d.out, (unsigned)(npix * d.Cout * 2));
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         const int co = cw0 + 8 * gq + 4 * hh;
         const bool cok = co < d.Cout;
-        float sc4[4] = {0.f, 0.f, 0.f, 0.f}, sf4[4] = {0.f, 0.f, 0.f, 0.f};
-        if (cok && d.bnb_relu) {
-          const float4 a4 = *reinterpret_cast<const float4*>(d.bnb_scale + co);
-          const float4 b4 = *reinterpret_cast<const float4*>(d.bnb_shift + co);
-          sc4[0] = a4.x; sc4[1] = a4.y; sc4[2] = a4.z; sc4[3] = a4.w;
-          sf4[0] = b4.x; sf4[1] = b4.y; sf4[2] = b4.z; sf4[3] = b4.w;
-        }
+        const int cb = co - (int)blockIdx.y * C5_BN;
+        const float4 a4 = *reinterpret_cast<const float4*>(btab + cb);
+        const float4 b4 = *reinterpret_cast<const float4*>(btab + C5_BN + cb);
+        const float sc4[4] = {a4.x, a4.y, a4.z, a4.w}, sf4[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const unsigned pix = pix0 + (unsigned)i * d.W;
-          if (colok && i < rows && cok) {
-            uint2 pk;
-            pk.x = pack2_16<T>(acc[i][4 * gq], acc[i][4 * gq + 1]);
-            pk.y = pack2_16<T>(acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
-            *reinterpret_cast<uint2*>(y + (size_t)pix * d.Cout + co) = pk;
+          const bool ok = colok && i < rows && cok;
+          uint2 pk;
+          pk.x = pack2_16<T>(acc[i][4 * gq], acc[i][4 * gq + 1]);
+          pk.y = pack2_16<T>(acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
+          const unsigned vo = ok ? (pix * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
+          typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), rg, (int)vo, 0, 0);
+          if (ok) {
             float gv[4], yy[4];
             unpack4_16<T>(pk, gv);
             unpack4_16<T>(yv[i][gq], yy);
@@ -467,7 +527,27 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
           }
         }
       }
-    } else {  // OM5_F32
+      issue_next();     // the last chunk's DMA, deferred behind the y1 wait
+      sw = 1;           // the next chunk's wait leaves the NST stores (older than that DMA) in flight
+    } else if (f32_counted) {  // OM5_F32, plain stores: buffer stores, fixed count NST (sw as the y epilogue)
+      const int c2 = d.Cout - d.split;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const unsigned pix = pix0 + (unsigned)i * d.W;
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int co = cw0 + 8 * gq + 4 * hh;
+          const bool to1 = cw0 + 8 * gq < d.split;     // wave-uniform (split % 8 == 0)
+          const bool ok = colok && i < rows && co < d.Cout;
+          const unsigned vo = !ok ? OOB : to1 ? (pix * (unsigned)d.split + (unsigned)co) * 4u
+                                             : (pix * (unsigned)c2 + (unsigned)(co - d.split)) * 4u;
+          typedef __attribute__((ext_vector_type(4))) float f32x4v;
+          const f32x4v w = {acc[i][4 * gq], acc[i][4 * gq + 1], acc[i][4 * gq + 2], acc[i][4 * gq + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, w), to1 ? rf1 : rf2, (int)vo, 0, 0);
+        }
+      }
+      sw = 2;
+    } else {  // OM5_F32 with read-modify-write (accumulating into an existing gradient)
       float* o1 = (float*)d.out;
       float* o2 = (float*)d.out2;
       const int c2 = d.Cout - d.split;

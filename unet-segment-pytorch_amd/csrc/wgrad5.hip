@@ -29,7 +29,7 @@
 
 namespace unet {
 
-constexpr int W5_TH = 2, W5_TW = 32, W5_HW = 34, W5_NW = 8, W5_NT = 512;
+constexpr int W5_TW = 32, W5_HW = 34, W5_NW = 8, W5_NT = 512;
 int slab_reduce_two_pass(const float* ws, int splits, long long total, float* scratch, float* dw, int accum,
                          hipStream_t st);                                                   // pw.hip
 int wgrad_reduce2_launch(const float* ws, int splits, long long total, float* dw, int accum, hipStream_t st);  // wgrad2.hip
@@ -45,11 +45,11 @@ __device__ __forceinline__ int w5_swz(int x) {
   else return 2 * ((x >> 1) & 1) + 4 * ((x >> 3) & 1);
 }
 
-template <int UPPD, int UPPX, bool ACT>
+template <int TH, int UPPD, int UPPX, bool ACT>
 struct W5Layout {
-  static constexpr int DUN = W5_TH * W5_TW * UPPD;        // dy image: 16-byte units
+  static constexpr int DUN = TH * W5_TW * UPPD;        // dy image: 16-byte units
   static constexpr int NID = DUN / 64;                     // DMA instructions per dy image (exact)
-  static constexpr int XPIX = (W5_TH + 2) * W5_HW;
+  static constexpr int XPIX = (TH + 2) * W5_HW;
   static constexpr int XUN = XPIX * UPPX;
   static constexpr int NIX = (XUN + 63) / 64;
   static constexpr int DPWD = (NID + W5_NW - 1) / W5_NW, DPWX = (NIX + W5_NW - 1) / W5_NW;
@@ -74,16 +74,16 @@ __device__ __forceinline__ typename Mma<T>::frag w5_tr8(const unsigned char* r0,
 }
 
 // SK: SK_PLAIN (every source stored) or SK_ACT (src0 a BN activation, optionally gated; src1 stored)
-template <typename T, int WCO, int WK, int SK>
+template <typename T, int WCO, int WK, int SK, int TH>
 __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc d, int mtiles, int per_split,
                                                          float* ws) {
   constexpr int WCI = W5_NW / (WCO * WK);
   constexpr int BCO = 64 * WCO, BCI = 16 * WCI;
   constexpr int UPPD = BCO / 8, UPPX = BCI / 8;
   constexpr bool ACT = SK != SK_PLAIN;
-  using Lay = W5Layout<UPPD, UPPX, ACT>;
+  using Lay = W5Layout<TH, UPPD, UPPX, ACT>;
   constexpr int NID = Lay::NID, NIX = Lay::NIX, DPWD = Lay::DPWD, DPWX = Lay::DPWX;
-  constexpr int KPW = W5_TH / WK;            // K steps (rows) per wave per stage
+  constexpr int KPW = TH / WK;            // K steps (rows) per wave per stage
   constexpr int ND0 = DPWD + DPWX;           // DMA instructions per wave per stage (+ DPWX gate loads)
   __shared__ __attribute__((aligned(1024))) unsigned char lds[Lay::BYTES];
 
@@ -173,11 +173,11 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
   };
   auto cur_init = [&](Cur& c) {
     const int mt = mt0;
-    const int tiles_w = (d.W + W5_TW - 1) / W5_TW, tiles_h = (d.H + W5_TH - 1) / W5_TH;
+    const int tiles_w = (d.W + W5_TW - 1) / W5_TW, tiles_h = (d.H + TH - 1) / TH;
     c.t = 0; c.s3 = 0; c.s2 = 0;
     c.w0 = (mt % tiles_w) * W5_TW;
     const int t2 = mt / tiles_w;
-    c.h0 = (t2 % tiles_h) * W5_TH;
+    c.h0 = (t2 % tiles_h) * TH;
     c.n = t2 / tiles_h;
   };
   auto cur_next = [&](Cur& c) {
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
     c.w0 += W5_TW;
     if (c.w0 >= d.W) {
       c.w0 = 0;
-      c.h0 += W5_TH;
+      c.h0 += TH;
       if (c.h0 >= d.H) { c.h0 = 0; ++c.n; }
     }
   };
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
 // ------------------------------------------------------------------------------------------------
 struct W5Plan {
   bool ok;
-  int wco, wk, mtiles, splits, per_split;
+  int wco, wk, th, mtiles, splits, per_split;
   size_t ws_bytes;
 };
 
@@ -415,7 +415,10 @@ static W5Plan wgrad5_plan(const unet_wgrad_desc* d) {
   p.wco = d->Cout >= 128 ? 2 : 1;
   p.wk = d->Cout >= 128 ? 1 : 2;
   const int bco = 64 * p.wco, bci = 64;
-  p.mtiles = d->N * cdiv(d->W, W5_TW) * cdiv(d->H, W5_TH);
+  // 4-row stages where the LDS allows (stored sources, 64-channel output blocks): the halo rows cost 6/4
+  // instead of 4/2 of a stage's rows and each wave runs two K steps per stage
+  p.th = (d->src[0].kind == UNET_SRC_PLAIN && p.wco == 1) ? 4 : 2;
+  p.mtiles = d->N * cdiv(d->W, W5_TW) * cdiv(d->H, p.th);
   const long long tiles_out = (long long)(d->Cout / bco) * (d->Cin / bci);
   const size_t slab = (size_t)d->Cout * d->Cin * 9 * sizeof(float);
   // one resident block per CU: at least 256 blocks, the split count a multiple of 8 (the blocks of one
@@ -437,16 +440,19 @@ bool wgrad5_eligible(const unet_wgrad_desc* d, size_t* ws_bytes) {
   if (mode == 0) return false;
   const W5Plan p = wgrad5_plan(d);
   if (!p.ok) return false;
-  // default: pipelines of >= 6 stages per block (short ones are prologue-bound; wgrad2 keeps those)
+  // default: pipelines of >= 6 stages per block (short ones are prologue-bound; wgrad2 keeps those), and not
+  // for a BN-activation source feeding a 64-channel output (2-row stages with the in-LDS transform: wgrad2
+  // measured 9-15 % faster there; the stored-source form of those layers runs 4-row stages and wins by 20 %)
   if (mode == 2 && p.per_split < 6) return false;
+  if (mode == 2 && d->src[0].kind == UNET_SRC_ACT && p.wco == 1) return false;
   if (ws_bytes) *ws_bytes = p.ws_bytes;
   return true;
 }
 
-template <typename T, int WCO, int WK, int SK>
+template <typename T, int WCO, int WK, int SK, int TH>
 static int launch5w(const unet_wgrad_desc* d, const W5Plan& p, hipStream_t st) {
   dim3 grid(p.splits, d->Cin / 64, d->Cout / (64 * WCO));
-  hipLaunchKernelGGL((wgrad5_kernel<T, WCO, WK, SK>), grid, dim3(W5_NT), 0, st, *d, p.mtiles, p.per_split,
+  hipLaunchKernelGGL((wgrad5_kernel<T, WCO, WK, SK, TH>), grid, dim3(W5_NT), 0, st, *d, p.mtiles, p.per_split,
                      (float*)d->workspace);
   return check_launch("wgrad5");
 }
@@ -454,8 +460,8 @@ static int launch5w(const unet_wgrad_desc* d, const W5Plan& p, hipStream_t st) {
 template <typename T>
 static int dispatch5w(const unet_wgrad_desc* d, const W5Plan& p, hipStream_t st) {
   const bool act = d->src[0].kind == UNET_SRC_ACT;
-  if (p.wco == 2) return act ? launch5w<T, 2, 1, SK_ACT>(d, p, st) : launch5w<T, 2, 1, SK_PLAIN>(d, p, st);
-  return act ? launch5w<T, 1, 2, SK_ACT>(d, p, st) : launch5w<T, 1, 2, SK_PLAIN>(d, p, st);
+  if (p.wco == 2) return act ? launch5w<T, 2, 1, SK_ACT, 2>(d, p, st) : launch5w<T, 2, 1, SK_PLAIN, 2>(d, p, st);
+  return act ? launch5w<T, 1, 2, SK_ACT, 2>(d, p, st) : launch5w<T, 1, 2, SK_PLAIN, 4>(d, p, st);
 }
 
 int wgrad5_run(const unet_wgrad_desc* d, hipStream_t st) {

@@ -83,9 +83,12 @@ class ConvBN:
         d.out_mode = L.OUT_Y
         d.out = y.data_ptr()
         # the weight gradient's input: src[0] is a BN activation (+gate) that this forward transforms anyway;
-        # where the kernel can write it once (act_out), the wgrad reads that stored map instead
+        # where the kernel can write it once (act_out), the wgrad reads that stored map instead.  Maps up to
+        # 256^2 only: on the 512^2 64-channel layers the forward is already near its HBM time (read x, write
+        # y), and the extra 2-byte-per-element write cost as much there (+50 us) as the wgrad saves
+        # (profiles/r03_layerprof_act_out.txt)
         self.wsrcs = self.wact = None
-        if training and srcs[0].kind == L.SRC_ACT and not os.environ.get("UNET_NO_ACT_OUT") \
+        if training and srcs[0].kind == L.SRC_ACT and H * W <= 256 * 256 and not os.environ.get("UNET_NO_ACT_OUT") \
                 and L.load().unet_conv_act_out_ok(d):
             act = torch.empty(N, H, W, srcs[0].C, dtype=prec.torch_dtype, device=dev)
             d.act_out = act.data_ptr()
