@@ -6,6 +6,7 @@ export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests/test_gpu_conv4.py tests/test_gpu_wgrad5.py tests/test_gpu_fusion_equivalence.py tests/test_gpu_ops.py -k "conv4 or conv5 or wgrad or act_out or fused or bn_backward_sums or conv_fwd or conv_dgrad or bench_tiles or pw_" -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -2 $O/tests.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/tests.log | head -20; exit 1; }
+for w in 1 0; do WG_KIND=act UNET_WGRAD5=$w timeout -k 10 60 python tools/wgrad_one.py 4 512 512 64 64 20 > $O/one.log 2>&1 || { tail -5 $O/one.log; exit 1; }; tail -1 $O/one.log; done
 timeout -k 10 200 python -u tools/layerprof.py > $O/layerprof.txt 2>&1 || { echo "layerprof failed"; tail -20 $O/layerprof.txt; exit 1; }
 UNET_CONV5=1 timeout -k 10 200 python -u tools/layerprof.py > $O/layerprof_c5.txt 2>&1 || { echo "layerprof failed"; tail -20 $O/layerprof_c5.txt; exit 1; }
 grep -A8 "per entry point" $O/layerprof.txt

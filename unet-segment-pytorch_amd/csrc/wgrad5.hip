@@ -33,7 +33,8 @@ constexpr int W5_TW = 32, W5_HW = 34, W5_NW = 8, W5_NT = 512;
 int slab_reduce_two_pass(const float* ws, int splits, long long total, float* scratch, float* dw, int accum,
                          hipStream_t st);                                                   // pw.hip
 int wgrad_reduce2_launch(const float* ws, int splits, long long total, float* dw, int accum, hipStream_t st);  // wgrad2.hip
-constexpr int W5_RG = 32, W5_RG_MIN = 32;   // as wgrad2: two-pass slab reduction above 32 splits
+constexpr int W5_RG = 32, W5_RG_MIN = 32;   // as wgrad2: slab reduction scratch above 32 splits
+constexpr int W5_ACT_NG = 4;   // SK value of wgrad5 only: BN-activation source without the attention gate
 
 // XOR permutation of the 16-byte channel units of a pixel in column x (UPP units per pixel): the 8 columns a
 // half-wave's transposed read touches (x0 + {0..3, 8..11}) x 2 adjacent units land on 16 distinct bank
@@ -45,7 +46,7 @@ __device__ __forceinline__ int w5_swz(int x) {
   else return 2 * ((x >> 1) & 1) + 4 * ((x >> 3) & 1);
 }
 
-template <int TH, int UPPD, int UPPX, bool ACT>
+template <int TH, int UPPD, int UPPX, bool ACT, bool GT = ACT>
 struct W5Layout {
   static constexpr int DUN = TH * W5_TW * UPPD;        // dy image: 16-byte units
   static constexpr int NID = DUN / 64;                     // DMA instructions per dy image (exact)
@@ -60,7 +61,7 @@ struct W5Layout {
   static constexpr int OFF_X = OFF_D + 3 * DIMG;
   static constexpr int OFF_RAW = OFF_X + NCX * XIMG;
   static constexpr int OFF_GATE = OFF_RAW + (ACT ? 2 * XIMG : 0);
-  static constexpr int OFF_TAB = OFF_GATE + (ACT ? 2 * GATE : 0);
+  static constexpr int OFF_TAB = OFF_GATE + (GT ? 2 * GATE : 0);
   static constexpr int OFF_JUNK = OFF_TAB + (ACT ? 2 * UPPX * 8 * 4 : 0);
   static constexpr int BYTES = OFF_JUNK + 1024;
   static_assert(BYTES <= 160 * 1024, "LDS");
@@ -73,15 +74,16 @@ __device__ __forceinline__ typename Mma<T>::frag w5_tr8(const unsigned char* r0,
   return __builtin_bit_cast(typename Mma<T>::frag, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-// SK: SK_PLAIN (every source stored) or SK_ACT (src0 a BN activation, optionally gated; src1 stored)
+// SK: SK_PLAIN (every source stored), SK_ACT (src0 a BN activation, optionally gated; src1 stored) or W5_ACT_NG
+// (an ungated BN activation: no gate ring in LDS, which lets 4-row stages fit)
 template <typename T, int WCO, int WK, int SK, int TH>
 __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc d, int mtiles, int per_split,
                                                          float* ws) {
   constexpr int WCI = W5_NW / (WCO * WK);
   constexpr int BCO = 64 * WCO, BCI = 16 * WCI;
   constexpr int UPPD = BCO / 8, UPPX = BCI / 8;
-  constexpr bool ACT = SK != SK_PLAIN;
-  using Lay = W5Layout<TH, UPPD, UPPX, ACT>;
+  constexpr bool ACT = SK != SK_PLAIN, GT = SK == SK_ACT;
+  using Lay = W5Layout<TH, UPPD, UPPX, ACT, GT>;
   constexpr int NID = Lay::NID, NIX = Lay::NIX, DPWD = Lay::DPWD, DPWX = Lay::DPWX;
   constexpr int KPW = TH / WK;            // K steps (rows) per wave per stage
   constexpr int ND0 = DPWD + DPWX;           // DMA instructions per wave per stage (+ DPWX gate loads)
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
   const int cl0 = in1 ? ci0 - C0 : ci0;
   const int Cs = in1 ? s1.C : C0;
   const bool xact = ACT && !in1;
-  const bool gated = xact && s0.gate_p != nullptr;
+  const bool gated = GT && xact && s0.gate_p != nullptr;
   const long long npix = (long long)d.N * d.H * d.W;
   const rsrc4_t rsx = mk_rsrc4(in1 ? s1.data : s0.data, (unsigned)(npix * Cs * 2));
   const rsrc4_t rsd = mk_rsrc4(d.dy, (unsigned)(npix * d.Cout * 2));
@@ -417,7 +419,7 @@ static W5Plan wgrad5_plan(const unet_wgrad_desc* d) {
   const int bco = 64 * p.wco, bci = 64;
   // 4-row stages where the LDS allows (stored sources, 64-channel output blocks): the halo rows cost 6/4
   // instead of 4/2 of a stage's rows and each wave runs two K steps per stage
-  p.th = (d->src[0].kind == UNET_SRC_PLAIN && p.wco == 1) ? 4 : 2;
+  p.th = (p.wco == 1 && (d->src[0].kind == UNET_SRC_PLAIN || !d->src[0].gate_p)) ? 4 : 2;
   p.mtiles = d->N * cdiv(d->W, W5_TW) * cdiv(d->H, p.th);
   const long long tiles_out = (long long)(d->Cout / bco) * (d->Cin / bci);
   const size_t slab = (size_t)d->Cout * d->Cin * 9 * sizeof(float);
@@ -441,10 +443,10 @@ bool wgrad5_eligible(const unet_wgrad_desc* d, size_t* ws_bytes) {
   const W5Plan p = wgrad5_plan(d);
   if (!p.ok) return false;
   // default: pipelines of >= 6 stages per block (short ones are prologue-bound; wgrad2 keeps those), and not
-  // for a BN-activation source feeding a 64-channel output (2-row stages with the in-LDS transform: wgrad2
-  // measured 9-15 % faster there; the stored-source form of those layers runs 4-row stages and wins by 20 %)
+  // for a gated BN-activation source feeding a 64-channel output (its gate ring leaves room for 2-row stages
+  // only, where wgrad2 measured 9-15 % faster; the ungated and stored sources run 4-row stages)
   if (mode == 2 && p.per_split < 6) return false;
-  if (mode == 2 && d->src[0].kind == UNET_SRC_ACT && p.wco == 1) return false;
+  if (mode == 2 && d->src[0].kind == UNET_SRC_ACT && d->src[0].gate_p && p.wco == 1) return false;
   if (ws_bytes) *ws_bytes = p.ws_bytes;
   return true;
 }
@@ -461,7 +463,8 @@ template <typename T>
 static int dispatch5w(const unet_wgrad_desc* d, const W5Plan& p, hipStream_t st) {
   const bool act = d->src[0].kind == UNET_SRC_ACT;
   if (p.wco == 2) return act ? launch5w<T, 2, 1, SK_ACT, 2>(d, p, st) : launch5w<T, 2, 1, SK_PLAIN, 2>(d, p, st);
-  return act ? launch5w<T, 1, 2, SK_ACT, 2>(d, p, st) : launch5w<T, 1, 2, SK_PLAIN, 4>(d, p, st);
+  if (!act) return launch5w<T, 1, 2, SK_PLAIN, 4>(d, p, st);
+  return d->src[0].gate_p ? launch5w<T, 1, 2, SK_ACT, 2>(d, p, st) : launch5w<T, 1, 2, W5_ACT_NG, 4>(d, p, st);
 }
 
 int wgrad5_run(const unet_wgrad_desc* d, hipStream_t st) {
