@@ -57,3 +57,20 @@ def test_graphed_predictor_copies():
     gp(x2)
     assert torch.equal(y1, y1c)                  # not overwritten by the next call
     assert gp(x2, copy=False) is gp.out
+
+
+def test_second_backward_raises():
+    """the per-module autograd nodes share one launch plan whose activation-gradient buffers are consumed by
+    the first backward: a second backward through the same forward (retain_graph=True) raises a clear
+    RuntimeError instead of re-using consumed buffers"""
+    from unet.models import AttentionUNet
+    from unet.utils.loss import DiceBCELoss
+    torch.manual_seed(0)
+    m = AttentionUNet(1, 2, base_features=8).cuda().train()
+    m.hip_precision = "bf16"
+    x = torch.rand(1, 1, 64, 64, device="cuda") * 2 - 1
+    t = (torch.rand(1, 64, 64, device="cuda") < 0.1).long()
+    loss = DiceBCELoss()(m(x), t)
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="second backward"):
+        loss.backward()

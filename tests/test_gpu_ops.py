@@ -918,3 +918,30 @@ def test_pw_dgrad_gated(shape, accum, prec):
     torch.cuda.synchronize()
     assert torch.equal(dq1, dq2) and torch.equal(part1, part2)
     assert torch.allclose(dx, dxs * s, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_pack_weights_batched_matches_single(prec):
+    """unet_pack_weights (one launch, LDS-tiled coalesced reads: csrc/pack.hip) writes exactly the packed
+    operands of the per-tensor unet_pack_weight for every job: 3x3 / 1x1, forward / transposed (dgrad), odd
+    channel counts (row padding to 128, partial 32-column chunks)"""
+    import ctypes
+    L, R = _lib(), _rt()
+    P = R._PRECISIONS[prec]
+    torch.manual_seed(21)
+    shapes = [(64, 64, 3), (40, 24, 3), (130, 64, 3), (32, 64, 1), (256, 512, 1), (1024, 512, 3), (64, 1, 3), (8, 33, 3)]
+    jobs, outs, refs = [], [], []
+    for co, ci, k in shapes:
+        w = torch.randn(co, ci, k, k, device="cuda")
+        for tr in (0, 1):
+            n = L.load().unet_packed_weight_elems(P.code, co, ci, k, tr)
+            o = torch.full((n,), 7.0, dtype=DT[prec], device="cuda")
+            r = R.pack_weight(w, P, transpose=bool(tr))
+            j = L.PackJob()
+            j.w, j.packed, j.Cout, j.Cin, j.ksize, j.transpose = w.data_ptr(), o.data_ptr(), co, ci, k, tr
+            jobs.append(j); outs.append((o, w)); refs.append(r)
+    arr = (L.PackJob * len(jobs))(*jobs)
+    L.call("unet_pack_weights", P.code, len(jobs), arr, R.stream())
+    torch.cuda.synchronize()
+    for (o, _), r in zip(outs, refs):
+        assert torch.equal(o.view(torch.int16), r.view(torch.int16))

@@ -121,13 +121,12 @@ def test_wgrad5_deterministic(shape, monkeypatch):
 
 def test_wgrad5_default_policy_at_bench_sizes(monkeypatch):
     """the default dispatch (UNET_WGRAD5 unset) at the bench's sizes: stored sources (the forward's act_out,
-    materialised pool / upsample), ungated BN activations and >= 128 output channels go to wgrad5; a gated
-    BN-activation source feeding a 64-channel output stays on wgrad2 (measured faster there)"""
+    materialised pool / upsample), BN activations (gated or not) and >= 128 output channels all go to wgrad5"""
     monkeypatch.delenv("UNET_WGRAD5", raising=False)
     L, R = _lib(), _rt()
     for shape, kind, want in [((4, 512, 512, 64, 64), "plain", "wgrad5"), ((4, 512, 512, 128, 64), "plain", "wgrad5"),
                               ((4, 256, 256, 128, 128), "gated+plain", "wgrad5"),
-                              ((4, 512, 512, 64, 64), "act", "wgrad5"), ((4, 512, 512, 128, 64), "gated+plain", "wgrad2")]:
+                              ((4, 512, 512, 64, 64), "act", "wgrad5"), ((4, 512, 512, 128, 64), "gated+plain", "wgrad5")]:
         srcs, x, dy, keep = _case(shape, kind, torch.bfloat16)
         N, H, W, cin, cout = shape
         wd = L.WgradDesc()

@@ -485,6 +485,7 @@ static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t s
 template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
 bool conv5_eligible(const unet_conv_desc* d);   // conv5.hip: the LDS-DMA 3x3 path
 bool conv5_act_out_ok(const unet_conv_desc* d);
+int pack_tiles_launch(int dtype, int count, const unet_pack_job* jobs, hipStream_t st);   // pack.hip
 int conv5_run(const unet_conv_desc* d, hipStream_t st);
 int conv5_stats_rows(const unet_conv_desc* d);
 int conv5_variant(const unet_conv_desc* d, char* buf, int len);
@@ -673,6 +674,7 @@ int unet_pack_weights(int dtype, int count, const unet_pack_job* jobs, void* str
     const long long e = unet_packed_weight_elems(dtype, j.Cout, j.Cin, j.ksize, j.transpose);
     if (e > maxe) maxe = e;
   }
+  if (dtype != UNET_F32) return pack_tiles_launch(dtype, count, jobs, (hipStream_t)stream);   // pack.hip
   const long long maxu = maxe / (dtype != UNET_F32 ? 8 : 4);   // 16-byte units
   int blocks = (int)((maxu + 255) / 256);
   if (blocks > 1024) blocks = 1024;

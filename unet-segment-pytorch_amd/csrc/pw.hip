@@ -467,10 +467,19 @@ __global__ __launch_bounds__(256) void slab_reduce_q_kernel(const float* ws, int
 
 int slab_reduce_two_pass(const float* ws, int splits, long long total, float* scratch, float* dw, int accum,
                          hipStream_t st) {
-  (void)scratch;
   const long long total4 = total / 4;
-  hipLaunchKernelGGL(slab_reduce_q_kernel, dim3((unsigned)((total4 + 63) / 64)), dim3(256), 0, st, ws, splits, total4,
-                     dw, accum);
+  if (total4 >= 8192) {
+    hipLaunchKernelGGL(slab_reduce_q_kernel, dim3((unsigned)((total4 + 63) / 64)), dim3(256), 0, st, ws, splits, total4,
+                       dw, accum);
+    return check_launch("slab_reduce");
+  }
+  // small weights (the attention gate's 1x1 projections): too few columns for one launch to fill the chip —
+  // splits -> PW_RG groups -> 1, still a fixed order
+  const int per = cdiv(splits, PW_RG), groups = cdiv(splits, per);
+  hipLaunchKernelGGL(pw_slab_reduce_kernel, dim3(cdiv(total4, 256), groups), dim3(256), 0, st, ws, splits, per, total4,
+                     scratch, 0);
+  hipLaunchKernelGGL(pw_slab_reduce_kernel, dim3(cdiv(total4, 256), 1), dim3(256), 0, st, (const float*)scratch, groups,
+                     groups, total4, dw, accum);
   return check_launch("slab_reduce");
 }
 static bool pw_src_ok(const unet_src& s, int C) {

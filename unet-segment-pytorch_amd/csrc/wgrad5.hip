@@ -56,7 +56,8 @@ struct W5Layout {
   static constexpr int DPWD = (NID + W5_NW - 1) / W5_NW, DPWX = (NIX + W5_NW - 1) / W5_NW;
   static constexpr int DIMG = NID * 1024, XIMG = NIX * 1024;
   static constexpr int NCX = ACT ? 2 : 3;                  // compute-image ring of the halo
-  static constexpr int GATE = NIX * 256;                   // one fp32 gate pre-activation per DMA lane slot
+  // gate pre-activations: per wave one 64-lane DMA of the (<= 8 per instruction) pixels its halo slots cover
+  static constexpr int GATE = W5_NW * 256;
   static constexpr int OFF_D = 0;
   static constexpr int OFF_X = OFF_D + 3 * DIMG;
   static constexpr int OFF_RAW = OFF_X + NCX * XIMG;
@@ -75,7 +76,7 @@ __device__ __forceinline__ typename Mma<T>::frag w5_tr8(const unsigned char* r0,
 }
 
 // SK: SK_PLAIN (every source stored), SK_ACT (src0 a BN activation, optionally gated; src1 stored) or W5_ACT_NG
-// (an ungated BN activation: no gate ring in LDS, which lets 4-row stages fit)
+// (an ungated BN activation: no gate ring in LDS)
 template <typename T, int WCO, int WK, int SK, int TH>
 __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc d, int mtiles, int per_split,
                                                          float* ws) {
@@ -142,6 +143,17 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
     xrow[k] = u < Lay::XUN ? hp / W5_HW - 1 : -(1 << 16);
     xcol[k] = hx - 1;
     xch[k] = 8 * ((u % UPPX) ^ w5_swz<UPPX>(hx));
+  }
+
+  // the gate DMA lane: lane 8k + p loads the pre-activation of pixel p of this wave's k-th halo instruction
+  // (instruction i = wave + 8k covers units 64 i .. 64 i + 63, i.e. pixels 8 i .. 8 i + 7 at 8 units per pixel)
+  static_assert(!GT || UPPX == 8, "gate layout assumes 8 units per halo pixel");
+  int grow, gcol;
+  {
+    const int k = lane >> 3, i = wave + k * W5_NW, hp = 8 * i + (lane & 7);
+    const bool v = k < DPWX && i < NIX && hp < Lay::XPIX;
+    grow = v ? hp / W5_HW - 1 : -(1 << 16);
+    gcol = hp % W5_HW - 1;
   }
 
   // ---- transposed-read addresses (bytes inside an image; + row * row stride as an immediate) ----
@@ -216,15 +228,10 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
       dma16(rsx, i < NIX ? ximg + i * 1024 : junk, ok ? (pix * (unsigned)Cs + (unsigned)(cl0 + xch[k])) * 2u : OOB);
     }
     if (gated) {
-      const unsigned gd = l32 + Lay::OFF_GATE + c.s2 * Lay::GATE;
-#pragma unroll
-      for (int k = 0; k < DPWX; ++k) {
-        const int i = wave + k * W5_NW;
-        const int y = c.h0 + xrow[k], x = c.w0 + xcol[k];
-        const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
-        const unsigned pix = pb + (unsigned)(xrow[k] * d.W + xcol[k]);
-        dma4(rsg, i < NIX ? gd + i * 256 : junk, ok ? pix * 4u : OOB);
-      }
+      const int y = c.h0 + grow, x = c.w0 + gcol;
+      const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
+      const unsigned pix = pb + (unsigned)(grow * d.W + gcol);
+      dma4(rsg, l32 + Lay::OFF_GATE + c.s2 * Lay::GATE + wave * 256, ok ? pix * 4u : OOB);
     }
   };
 
@@ -252,7 +259,8 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
           const float sf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
           float gm = ok ? 1.f : 0.f;
           if (gated) {
-            const float pv = *reinterpret_cast<const float*>(lds + Lay::OFF_GATE + c.s2 * Lay::GATE + i * 256 + lane * 4);
+            const float pv = *reinterpret_cast<const float*>(lds + Lay::OFF_GATE + c.s2 * Lay::GATE + wave * 256 +
+                                                             (k * 8 + (lane >> 3)) * 4);
             gm = ok ? sigmoidf_(pv * ga + gb) : 0.f;
           }
           float v[8];
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
   if (ntl > 1) {
     issue(I);
     cur_next(I);
-    if (gated) wait_vm<ND0 + DPWX>(); else wait_vm<ND0>();
+    if (gated) wait_vm<ND0 + 1>(); else wait_vm<ND0>();
   } else {
     wait_vm<0>();
   }
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
   // this wave's DMAs of the stage after K have landed (only the youngest stage's may still be in flight)
   auto wait_next = [&](int t) {
     if (t + 2 < ntl) {
-      if (gated) wait_vm<ND0 + DPWX>(); else wait_vm<ND0>();
+      if (gated) wait_vm<ND0 + 1>(); else wait_vm<ND0>();
     } else {
       wait_vm<0>();
     }
@@ -419,7 +427,7 @@ static W5Plan wgrad5_plan(const unet_wgrad_desc* d) {
   const int bco = 64 * p.wco, bci = 64;
   // 4-row stages where the LDS allows (stored sources, 64-channel output blocks): the halo rows cost 6/4
   // instead of 4/2 of a stage's rows and each wave runs two K steps per stage
-  p.th = (p.wco == 1 && (d->src[0].kind == UNET_SRC_PLAIN || !d->src[0].gate_p)) ? 4 : 2;
+  p.th = p.wco == 1 ? 4 : 2;
   p.mtiles = d->N * cdiv(d->W, W5_TW) * cdiv(d->H, p.th);
   const long long tiles_out = (long long)(d->Cout / bco) * (d->Cin / bci);
   const size_t slab = (size_t)d->Cout * d->Cin * 9 * sizeof(float);
@@ -442,11 +450,8 @@ bool wgrad5_eligible(const unet_wgrad_desc* d, size_t* ws_bytes) {
   if (mode == 0) return false;
   const W5Plan p = wgrad5_plan(d);
   if (!p.ok) return false;
-  // default: pipelines of >= 6 stages per block (short ones are prologue-bound; wgrad2 keeps those), and not
-  // for a gated BN-activation source feeding a 64-channel output (its gate ring leaves room for 2-row stages
-  // only, where wgrad2 measured 9-15 % faster; the ungated and stored sources run 4-row stages)
+  // default: pipelines of >= 6 stages per block (short ones are prologue-bound; wgrad2 keeps those)
   if (mode == 2 && p.per_split < 6) return false;
-  if (mode == 2 && d->src[0].kind == UNET_SRC_ACT && d->src[0].gate_p && p.wco == 1) return false;
   if (ws_bytes) *ws_bytes = p.ws_bytes;
   return true;
 }
@@ -464,7 +469,7 @@ static int dispatch5w(const unet_wgrad_desc* d, const W5Plan& p, hipStream_t st)
   const bool act = d->src[0].kind == UNET_SRC_ACT;
   if (p.wco == 2) return act ? launch5w<T, 2, 1, SK_ACT, 2>(d, p, st) : launch5w<T, 2, 1, SK_PLAIN, 2>(d, p, st);
   if (!act) return launch5w<T, 1, 2, SK_PLAIN, 4>(d, p, st);
-  return d->src[0].gate_p ? launch5w<T, 1, 2, SK_ACT, 2>(d, p, st) : launch5w<T, 1, 2, W5_ACT_NG, 4>(d, p, st);
+  return d->src[0].gate_p ? launch5w<T, 1, 2, SK_ACT, 4>(d, p, st) : launch5w<T, 1, 2, W5_ACT_NG, 4>(d, p, st);
 }
 
 int wgrad5_run(const unet_wgrad_desc* d, hipStream_t st) {
