@@ -345,7 +345,7 @@ def main():
         tr = json.loads(tfile.read_text())
         ent = tr.get(f"{target}@{args.size}x{args.in_ch}") or tr.get(target)
         traffic = ent.get("bytes_per_launch") if isinstance(ent, dict) else ent
-    headline = (args.size, args.in_ch, args.accum) == (512, 1, 1)
+    headline = (args.size, args.in_ch, args.accum, args.model) == (512, 1, 1, "attention_unet")
     metric = METRIC if headline else (
         f"{args.size}x{args.size} {args.in_ch}-ch slices/sec fwd+bwd, {'AttentionUNet' if args.model == 'attention_unet' else 'UNet'} "
         f"bs={args.batch}/GPU x grad-accum {args.accum}, {args.precision}, 1/2/4/8 MI355X")
