@@ -4,6 +4,8 @@ of scope."""
 
 from .loss import DiceLoss, BalancedCELoss, DiceBCELoss, DeepSupervisionLoss, create_loss_function
 from .metrics import SegmentationMetrics, compute_dice, compute_iou
+from .config import load_config, create_model, create_criterion, build_from_config
 
 __all__ = ["DiceLoss", "BalancedCELoss", "DiceBCELoss", "DeepSupervisionLoss", "create_loss_function",
-           "SegmentationMetrics", "compute_iou", "compute_dice"]
+           "SegmentationMetrics", "compute_iou", "compute_dice", "load_config", "create_model", "create_criterion",
+           "build_from_config"]
