@@ -436,26 +436,30 @@ def test_outconv_bwd_vec(shape, accum):
 
 
 @pytest.mark.parametrize("geo", [(2, 32, 32, 64, 64, 64), (1, 16, 20, 33, 41, 32), (2, 7, 9, 14, 18, 8),
-                                 (1, 25, 17, 50, 34, 12)])
+                                 (1, 25, 17, 50, 34, 12), (4, 256, 256, 512, 512, 64), (2, 32, 32, 64, 64, 512),
+                                 (1, 13, 37, 27, 75, 48)])
 @pytest.mark.parametrize("accum", [0, 1])
 def test_upsample_bwd(geo, accum):
-    """Adjoint of bilinear x2 (align_corners=True) + F.pad into the skip's frame (layers.py:78,98-102)."""
+    """Adjoint of bilinear x2 (align_corners=True) + F.pad into the skip's frame (layers.py:78,98-102),
+    incl. the bench's 256^2 -> 512^2 x 64-channel case, against torch's adjoint in fp64"""
     L, R = _lib(), _rt()
     N, h, w, Hp, Wp, C = geo
     up_h, up_w = 2 * h, 2 * w
     pt, pl = (Hp - up_h) // 2, (Wp - up_w) // 2
     torch.manual_seed(9)
     g = torch.randn(N, Hp, Wp, C, device="cuda")
-    x = torch.randn(N, C, h, w, device="cuda", requires_grad=True)
+    # reference: torch's adjoint in fp64 (its fp32 form scatters with atomics: order-dependent rounding)
+    x = torch.randn(N, C, h, w, device="cuda", dtype=torch.float64, requires_grad=True)
     u = F.interpolate(x, size=(up_h, up_w), mode="bilinear", align_corners=True)
     u = F.pad(u, [pl, Wp - up_w - pl, pt, Hp - up_h - pt])
-    u.backward(g.permute(0, 3, 1, 2))
+    u.backward(g.double().permute(0, 3, 1, 2))
     ref = x.grad.permute(0, 2, 3, 1)
     dx = torch.full((N, h, w, C), 1.5, device="cuda")
     L.call("unet_upsample_bwd", N, C, h, w, up_h, up_w, pt, pl, Hp, Wp, R.up_scale(h, up_h), R.up_scale(w, up_w),
            g.data_ptr(), dx.data_ptr(), accum, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    assert ((dx - 1.5 * accum) - ref).abs().max() <= 1e-5 * (1 + ref.abs().max())
+    err = float(((dx - 1.5 * accum).double() - ref).abs().max())
+    assert err <= 1e-5 * (1 + float(ref.abs().max())), err
 
 
 # ------------------------------------------------------------------------------------------------
