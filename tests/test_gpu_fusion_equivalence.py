@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 def _grads(model, x, t, env, seen=None):
     from unet._hip import lib as L
     from unet.utils.loss import DiceBCELoss
-    old = {k: os.environ.get(k) for k in ("UNET_NO_POOL_FOLD", "UNET_NO_GATE_FUSE", "UNET_NO_ACT_OUT", "UNET_NO_OC_FUSE")}
+    old = {k: os.environ.get(k) for k in ("UNET_NO_POOL_FOLD", "UNET_NO_GATE_FUSE", "UNET_NO_ACT_OUT", "UNET_NO_OC_FUSE",
+                                         "UNET_NO_GATE_VEC")}
     orig = L.call
 
     def rec(name, *args):
@@ -134,6 +135,40 @@ def test_outconv_bn_backward_fused(prec, kind):
         # BatchNorm's scalar parameters are sums with heavy cancellation (the BN-sums fusion's own test sees
         # the same: all params rel-L2 6e-3, worst tensor 5e-2) — gate the whole gradient and each tensor's
         # largest deviation
+        a = torch.cat([g0[n].double().flatten() for n in g0])
+        b = torch.cat([g1[n].double().flatten() for n in g0])
+        assert float((a - b).norm() / b.norm()) <= 1e-2
+        for n in g0:
+            d = float((g0[n].double() - g1[n].double()).abs().max() / (g1[n].double().abs().max() + 1e-30))
+            assert d <= 0.1, (n, d)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("base,size", [(16, 96), (64, 128)])
+def test_gate_vec_passes_equivalent(prec, base, size):
+    """Attention-gate backward passes 2 / 3 in the coalesced form (gate_bwd2_vec / gate_bwd3_vec: 8 channels
+    per lane) against the per-channel kernels (UNET_NO_GATE_VEC): pass 3 evaluates the same per-element
+    expressions, pass 2 sums the same terms in another fixed order — equal up to fp32 rounding (fp32 mode),
+    and up to the 16-bit roundings such a reorder can flip downstream (bf16 mode; gates as for the OutConv
+    fusion above)."""
+    from unet.models import AttentionUNet
+    torch.manual_seed(9)
+    m = AttentionUNet(1, 2, base_features=base).cuda().train()
+    m.hip_precision = prec
+    g = torch.Generator().manual_seed(10)
+    x = (torch.rand(2, 1, size, size + 32, generator=g) * 2 - 1).cuda()
+    t = (torch.rand(2, size, size + 32, generator=g) < 0.1).long().cuda()
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    out0, g0 = _grads(m, x, t, {})
+    m.load_state_dict(state)
+    out1, g1 = _grads(m, x, t, {"UNET_NO_GATE_VEC": "1"})
+    assert torch.equal(out0, out1)
+    if prec == "fp32":
+        for n in g0:
+            a, b = g0[n].double(), g1[n].double()
+            rel = float((a - b).norm() / (b.norm() + 1e-30))
+            assert rel <= 1e-4, (n, rel)
+    else:
         a = torch.cat([g0[n].double().flatten() for n in g0])
         b = torch.cat([g1[n].double().flatten() for n in g0])
         assert float((a - b).norm() / b.norm()) <= 1e-2

@@ -314,6 +314,123 @@ __global__ void gate_bwd3_kernel(long long P, int Ci, int CL, const T* gw, const
   }
 }
 
+// ---- coalesced gate passes 2 / 3 (Ci % 8 == 0, G = Ci/8 a power of two <= 64): a group of G lanes owns a
+// pixel, 8 channels per lane, so every load / store is one 16-byte vector (the per-channel forms above move
+// 2 bytes per lane).  Pass 2's four per-channel sums: per lane over its pixels, then xor-shuffles over the
+// lanes of a wave that hold the same channels, then the 4 waves in order through LDS — a fixed order
+// (deterministic), into the same [4][rows][Ci] partial layout, so unet_bn_bwd_finalize / unet_colsum are
+// unchanged.  Pass 3 evaluates the same per-element expressions as gate_bwd3_kernel (bit-identical).
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    store_vec<T>(p, v);
+  } else {
+    store_vec<float>((float*)p, v);
+    store_vec<float>((float*)p + 4, v + 4);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gate_bwd2_vec_kernel(long long P, int Ci, int G, const T* gw, const T* xw,
+                                                            const float* gab, const float* xab, const float* gm,
+                                                            const float* gi, const float* xm, const float* xi,
+                                                            const float* wpsi, const float* dq, const float* pp,
+                                                            const float* pc, float* part, int rows) {
+  __shared__ float sh[4][4][256];   // [wave][sum][channel], Ci <= 256 (G <= 32 for the partial width)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = lane % G, c0 = sub * 8, slots = 256 / G;
+  float gs[8], gb[8], xs[8], xb[8], gmu[8], giv[8], xmu[8], xiv[8], w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    gs[j] = gab[c]; gb[j] = gab[Ci + c]; xs[j] = xab[c]; xb[j] = xab[Ci + c];
+    gmu[j] = gm[c]; giv[j] = gi[c]; xmu[j] = xm[c]; xiv[j] = xi[c]; w[j] = wpsi[c];
+  }
+  const float A = pc[0], B = pc[1], Cc = pc[2];
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  float a0[8], a1[8], a2[8], a3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { a0[j] = 0.f; a1[j] = 0.f; a2[j] = 0.f; a3[j] = 0.f; }
+  for (long long q = p0 + tid / G; q < p1; q += slots) {
+    float g[8], x[8];
+    load8<T>(gw + q * Ci + c0, g);
+    load8<T>(xw + q * Ci + c0, x);
+    const float dp = A * dq[q] + B * pp[q] + Cc;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = fmaxf(g[j] * gs[j] + gb[j] + x[j] * xs[j] + xb[j], 0.f);
+      const float dz = a > 0.f ? dp * w[j] : 0.f;
+      a0[j] += dz;
+      a1[j] += dz * (g[j] - gmu[j]) * giv[j];
+      a2[j] += dz * (x[j] - xmu[j]) * xiv[j];
+      a3[j] += dp * a;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    for (int o = G; o < 64; o <<= 1) {
+      a0[j] += __shfl_xor(a0[j], o, 64);
+      a1[j] += __shfl_xor(a1[j], o, 64);
+      a2[j] += __shfl_xor(a2[j], o, 64);
+      a3[j] += __shfl_xor(a3[j], o, 64);
+    }
+    if (lane < G) {
+      sh[wave][0][c0 + j] = a0[j];
+      sh[wave][1][c0 + j] = a1[j];
+      sh[wave][2][c0 + j] = a2[j];
+      sh[wave][3][c0 + j] = a3[j];
+    }
+  }
+  __syncthreads();
+  if (tid < Ci) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+      part[((size_t)f * rows + blockIdx.x) * Ci + tid] = ((sh[0][f][tid] + sh[1][f][tid]) + sh[2][f][tid]) + sh[3][f][tid];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gate_bwd3_vec_kernel(long long P, int Ci, int G, const T* __restrict__ gw, const T* __restrict__ xw,
+                                                            const float* gab, const float* xab, const float* wpsi,
+                                                            const float* __restrict__ dq, const float* __restrict__ pp, const float* pc,
+                                                            const float* gcoef, const float* xcoef, T* __restrict__ dgw, T* __restrict__ dxw,
+                                                            int rows) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int sub = lane % G, c0 = sub * 8, slots = 256 / G;
+  float gs[8], gb[8], xs[8], xb[8], w[8], gA[8], gB[8], gC[8], xA[8], xB[8], xC[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    gs[j] = gab[c]; gb[j] = gab[Ci + c]; xs[j] = xab[c]; xb[j] = xab[Ci + c]; w[j] = wpsi[c];
+    gA[j] = gcoef[c]; gB[j] = gcoef[Ci + c]; gC[j] = gcoef[2 * Ci + c];
+    xA[j] = xcoef[c]; xB[j] = xcoef[Ci + c]; xC[j] = xcoef[2 * Ci + c];
+  }
+  const float A = pc[0], B = pc[1], Cc = pc[2];
+  const long long per = (P + rows - 1) / rows;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  for (long long q = p0 + tid / G; q < p1; q += slots) {
+    float g[8], x[8], og[8], ox[8];
+    load8<T>(gw + q * Ci + c0, g);
+    load8<T>(xw + q * Ci + c0, x);
+    const float dp = A * dq[q] + B * pp[q] + Cc;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = fmaxf(g[j] * gs[j] + gb[j] + x[j] * xs[j] + xb[j], 0.f);
+      const float dz = a > 0.f ? dp * w[j] : 0.f;
+      og[j] = gA[j] * dz + gB[j] * g[j] + gC[j];
+      ox[j] = xA[j] * dz + xB[j] * x[j] + xC[j];
+    }
+    store8<T>(dgw + q * Ci + c0, og);
+    store8<T>(dxw + q * Ci + c0, ox);
+  }
+}
+
+static bool gate_vec_ok(int Ci) {
+  const int G = vec_group(Ci);
+  return G && G <= 32 && !getenv("UNET_NO_GATE_VEC");
+}
+
 }  // namespace unet
 
 using namespace unet;
@@ -389,6 +506,17 @@ int unet_gate_bwd2(int dtype, long long P, int Ci, const void* gw, const void* x
                    const float* wpsi, const float* dq, const float* p, const float* psi_coef, float* partial,
                    void* stream) {
   const int cl = chan_lanes_g(Ci), rows = rows_for(P, Ci);
+  if (gate_vec_ok(Ci)) {
+    const int G = vec_group(Ci);
+#define UNET_G2V(TT)                                                                                                \
+  hipLaunchKernelGGL(gate_bwd2_vec_kernel<TT>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, G, (const TT*)gw, \
+                     (const TT*)xw, gab, xab, g_mean, g_invstd, x_mean, x_invstd, wpsi, dq, p, psi_coef, partial, rows)
+    if (dtype == UNET_F16) UNET_G2V(f16);
+    else if (dtype == UNET_BF16) UNET_G2V(bf16);
+    else UNET_G2V(float);
+#undef UNET_G2V
+    return check_launch("gate_bwd2");
+  }
   dim3 grid(cdiv(Ci, cl), rows);
   if (dtype == UNET_F16)
     hipLaunchKernelGGL(gate_bwd2_kernel<f16>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const f16*)gw,
@@ -409,6 +537,17 @@ int unet_gate_bwd3(int dtype, long long P, int Ci, const void* gw, const void* x
                    const float* wpsi, const float* dq, const float* p, const float* psi_coef, const float* gcoef,
                    const float* xcoef, void* dgw, void* dxw, void* stream) {
   const int cl = chan_lanes_g(Ci), rows = rows_for(P, Ci);
+  if (gate_vec_ok(Ci)) {
+    const int G = vec_group(Ci);
+#define UNET_G3V(TT)                                                                                                \
+  hipLaunchKernelGGL(gate_bwd3_vec_kernel<TT>, dim3(rows), dim3(256), 0, (hipStream_t)stream, P, Ci, G, (const TT*)gw, \
+                     (const TT*)xw, gab, xab, wpsi, dq, p, psi_coef, gcoef, xcoef, (TT*)dgw, (TT*)dxw, rows)
+    if (dtype == UNET_F16) UNET_G3V(f16);
+    else if (dtype == UNET_BF16) UNET_G3V(bf16);
+    else UNET_G3V(float);
+#undef UNET_G3V
+    return check_launch("gate_bwd3");
+  }
   dim3 grid(cdiv(Ci, cl), rows);
   if (dtype == UNET_F16)
     hipLaunchKernelGGL(gate_bwd3_kernel<f16>, grid, dim3(256), 0, (hipStream_t)stream, P, Ci, cl, (const f16*)gw,
