@@ -126,8 +126,9 @@ __device__ __forceinline__ void load8(const T* p, float* v) {
 }
 
 template <typename T>
-__global__ void psi_vec_kernel(long long P, int Ci, int G, const T* gw, const T* xw, const float* gab, const float* xab,
-                               const float* wpsi, float* p, float* part, int rows) {
+__global__ void psi_vec_kernel(long long P, int Ci, int G, const T* __restrict__ gw, const T* __restrict__ xw,
+                               const float* gab, const float* xab, const float* wpsi, float* __restrict__ p, float* part,
+                               int rows) {
   __shared__ float sh[8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int sub = lane % G, ppw = 64 / G;
@@ -162,11 +163,14 @@ __global__ void psi_vec_kernel(long long P, int Ci, int G, const T* gw, const T*
   }
 }
 
+constexpr int GB1_U = 4;   // pixels per lane per trip (loads in flight)
+
 template <typename T>
-__global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* dxs, const T* yx, const float* sx,
-                                     const float* bx, int relu, const float* pp, const float* psi_ab,
-                                     const float* psi_mean, const float* psi_inv, float* dx, int dx_accum, float* dq,
-                                     float* part, int rows) {
+__global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* __restrict__ dxs,
+                                     const T* __restrict__ yx, const float* sx, const float* bx, int relu,
+                                     const float* __restrict__ pp, const float* psi_ab, const float* psi_mean,
+                                     const float* psi_inv, float* __restrict__ dx, int dx_accum,
+                                     float* __restrict__ dq, float* part, int rows) {
   __shared__ float sh[8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int sub = lane % G, ppw = 64 / G;
@@ -178,15 +182,15 @@ __global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* dx
   const long long per = (P + rows - 1) / rows;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
   float s1 = 0.f, s2 = 0.f;
-  // two pixels per trip with every load issued before the stores (the stores to dx may alias the loads
+  // GB1_U pixels per trip with every load issued before the stores (the stores to dx may alias the loads
   // as far as the compiler knows, so a one-pixel loop serialises a full memory round trip per pixel);
   // s1 / s2 keep the one-pixel loop's pixel order
   const long long S = (long long)nw * ppw;
-  for (long long q = p0 + wave * ppw + lane / G; q < p1; q += 2 * S) {
-    float d[2][8], y[2][8], g[2][8], pv[2];
-    bool ok[2];
+  for (long long q = p0 + wave * ppw + lane / G; q < p1; q += GB1_U * S) {
+    float d[GB1_U][8], y[GB1_U][8], g[GB1_U][8], pv[GB1_U];
+    bool ok[GB1_U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < GB1_U; ++u) {
       ok[u] = q + u * S < p1;
       const long long qq = ok[u] ? q + u * S : q;
       load_vec<float>(dxs + qq * Cx + c0, d[u]);
@@ -199,7 +203,7 @@ __global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* dx
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < GB1_U; ++u) {
       const float sg = sigmoidf_(pv[u] * pa + pb);
       float ds = 0.f;
 #pragma unroll
