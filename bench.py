@@ -236,13 +236,14 @@ def main():
     backend = os.environ.get("UNET_DIST_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    # the device first: RCCL's communicator binds to the current device of the rank
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from unet._hip.runtime import probe
     from unet.models import AttentionUNet, UNet

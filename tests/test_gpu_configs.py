@@ -301,3 +301,53 @@ def test_c5_fp16_1024_vs_oracle(c5_ref):
     assert r_s <= 1.1 * r_a + 2e-2, (r_s, r_a)
     changed = sum(int(not torch.equal(p.detach(), before[k])) for k, p in m.named_parameters())
     assert changed == len(before)
+
+
+def test_c5_fp16_grad_accumulation_vs_oracle(c5_ref):
+    """C5 as configured trains with gradient accumulation under fp16 loss scaling (configs/lung_tumor.yaml:18,27;
+    scripts/train.py:133-143: loss / accum per micro-batch, backward, one unscale + step per accum group).  Two
+    micro-batches of 2 x 3 x 1024^2 through GradScaler: the unscaled accumulated gradients against the fp64
+    oracle's accumulated gradients, beside autocast-fp16's (same gate as the single micro-batch), and the scale
+    must be one at which every gradient of the group is finite."""
+    from fullsize_common import hip_model
+    from unet.utils.loss import DiceBCELoss
+    ref, f64a, aca = c5_ref, c5_ref["f64"], c5_ref["ac16"]
+    g = torch.Generator().manual_seed(2028)
+    x2 = torch.rand(2, 3, 1024, 1024, generator=g) * 2 - 1
+    t2 = discs(2, 1024, 1024, g)
+    f64b = oracle_run(ref["init"], x2, t2, "cuda", torch.float64, want_eval=False)
+    acb = oracle_run(ref["init"], x2, t2, "cuda", torch.float32, autocast=torch.float16, want_eval=False)
+    accum = 2
+    f64 = {k: (f64a["grads"][k] + f64b["grads"][k]) / accum for k in f64a["grads"]}
+    ac = {k: (aca["grads"][k] + acb["grads"][k]) / accum for k in aca["grads"]}
+    m = hip_model(ref["init"], "fp16", in_ch=3)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4)
+    scaler = torch.amp.GradScaler("cuda")
+    crit = DiceBCELoss()
+    batches = [(ref["x"].cuda(), ref["t"].cuda()), (x2.cuda(), t2.cuda())]
+    taken = False
+    for _ in range(6):
+        opt.zero_grad(set_to_none=True)
+        scale = scaler.get_scale()
+        losses = []
+        for x, t in batches:
+            loss = crit(m(x), t)
+            losses.append(float(loss.detach()))
+            scaler.scale(loss / accum).backward()
+        scaler.unscale_(opt)
+        sg = {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()}
+        finite = all(torch.isfinite(v).all() for v in sg.values())
+        scaler.step(opt)
+        scaler.update()
+        if finite:
+            taken = True
+            break
+        assert scaler.get_scale() < scale
+    assert taken
+    _, _, r_a = grad_errs(ac, f64)
+    w, k, r = grad_errs(sg, f64)
+    lrel = max(abs(a - b) / abs(b) for a, b in zip(losses, (f64a["loss"], f64b["loss"])))
+    print(f"\nC5 accum {accum} at scale {scale:.0f}: unscaled accumulated grads rel-L2 vs fp64 {r:.3e} "
+          f"(autocast-fp16 {r_a:.3e}), worst max-norm {w:.2e} ({k}); micro-batch losses rel {lrel:.1e}")
+    assert lrel <= 1e-2, lrel
+    assert r <= 1.1 * r_a + 2e-2 and r <= 0.7, (r, r_a)

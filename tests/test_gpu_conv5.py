@@ -1,6 +1,5 @@
-"""conv5 (csrc/conv5.hip: the LDS-DMA 3x3 conv on v_mfma_f32_32x32x16, the default path on large maps) and
-conv4 (csrc/conv4.hip: the register-staged 32x32x16 kernel, UNET_CONV5=0 UNET_CONV4=1) against torch fp32 on
-the same 16-bit operands, for every epilogue and source kind they serve, at bench sizes (the persistent multi-tile loop runs) and with
+"""conv5 (csrc/conv5.hip: the LDS-DMA 3x3 conv on v_mfma_f32_32x32x16, the default path on large maps)
+against torch fp32 on the same 16-bit operands, for every epilogue and source kind they serve, at bench sizes (the persistent multi-tile loop runs) and with
 partial tiles in both directions.  Reference ops: nn.Conv2d(k=3, pad=1, bias=False) forward
 (unet/models/layers.py:32,35) and its input gradient; BatchNorm2d forward partial sums / backward sums of
 the DoubleConv (layers.py:33,36).  Gates as the conv3 bench-tile tests: rel-L2 <= 4e-3, max-abs <= 2e-2 (1 +
@@ -18,16 +17,14 @@ Y_SHAPES = [(4, 512, 512, 64, 64), (4, 256, 256, 64, 128), (4, 256, 256, 128, 12
             (3, 200, 328, 64, 128), (8, 258, 98, 96, 64)]
 
 
-PATH = {"conv5": {"UNET_CONV5": "1", "UNET_CONV4": "0"}, "conv4": {"UNET_CONV5": "0", "UNET_CONV4": "1"}}
+PATH = {"conv5": {"UNET_CONV5": "1"}}
 
 
 def _want(prec, cout, path):
-    if path == "conv5":
-        return f"conv5_kernel<{TN[prec]},4>"
-    return f"conv4_kernel<{TN[prec]},4,2,1,4>" if cout <= 64 else f"conv4_kernel<{TN[prec]},2,4,1,4>"
+    return f"conv5_kernel<{TN[prec]},4>"
 
 
-@pytest.fixture(params=["conv5", "conv4"])
+@pytest.fixture(params=["conv5"])
 def path(request, monkeypatch):
     for k, v in PATH[request.param].items():
         monkeypatch.setenv(k, v)
@@ -37,7 +34,7 @@ def path(request, monkeypatch):
 @pytest.mark.parametrize("shape", Y_SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("src", ["plain", "act", "act_gate", "concat"])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv4_y_stats(prec, src, shape, path):
+def test_conv5_y_stats(prec, src, shape, path):
     L, R = _lib(), _rt()
     N, H, W, cin, cout = shape
     dt = DT[prec]
@@ -93,7 +90,7 @@ DGRAD_SHAPES = [(4, 512, 512, 128, 64), (4, 512, 512, 64, 64), (4, 256, 256, 256
 
 @pytest.mark.parametrize("shape", DGRAD_SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv4_dgrad_f32_split_accum(prec, shape, path):
+def test_conv5_dgrad_f32_split_accum(prec, shape, path):
     """dgrad of a forward conv cin -> cout: dy[cout] -> dx[cin], fp32, split across the concat with the first
     part accumulated (UNET_OUT_F32)."""
     L = _lib()
@@ -119,7 +116,7 @@ def test_conv4_dgrad_f32_split_accum(prec, shape, path):
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv4_matches_conv3(prec, path, monkeypatch):
+def test_conv5_matches_conv3(prec, path, monkeypatch):
     """The 32x32x16 kernels and conv3 on the same inputs agree to fp32 summation-order noise."""
     L = _lib()
     N, H, W, cin, cout = 4, 256, 256, 128, 128

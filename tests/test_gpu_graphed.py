@@ -74,3 +74,95 @@ def test_second_backward_raises():
     loss.backward(retain_graph=True)
     with pytest.raises(RuntimeError, match="second backward"):
         loss.backward()
+
+
+def _twins(base=16):
+    from unet.models import AttentionUNet
+    torch.manual_seed(0)
+    a = AttentionUNet(1, 2, base_features=base).cuda().train()
+    b = AttentionUNet(1, 2, base_features=base).cuda().train()
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        m.hip_precision = "bf16"
+    return a, b
+
+
+def _batches(n, size=128):
+    g = torch.Generator().manual_seed(5)
+    return [((torch.rand(2, 1, size, size, generator=g) * 2 - 1).cuda(),
+             (torch.rand(2, size, size, generator=g) < 0.1).long().cuda()) for _ in range(n)]
+
+
+def _eager_step(m, opt, crit, x, t):
+    opt.zero_grad(set_to_none=True)
+    loss = crit(m(x), t)
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(list(m.parameters()), 1.0)
+    opt.step()
+    return loss
+
+
+def test_graphed_train_step_with_live_eager_graph():
+    """VERDICT r03 'do this' 1: the caller keeps the last eager step's `loss` (and with it that step's autograd
+    graph and the parameters' AccumulateGrad nodes, created on the default stream) alive while it builds a
+    GraphedTrainStep on the same model.  Round 3's capture ran loss.backward() through those nodes and the
+    process died (segfault after torch's AccumulateGrad stream-mismatch warning).  Now: eager-identical steps."""
+    from unet.utils.graphed import GraphedTrainStep
+    from unet.utils.loss import DiceBCELoss
+    a, b = _twins()
+    oa = torch.optim.AdamW(a.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
+    ob = torch.optim.AdamW(b.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
+    crit = DiceBCELoss()
+    batches = _batches(4)
+    x0, t0 = batches[0]
+    la0 = _eager_step(a, oa, crit, x0, t0)
+    lb0 = _eager_step(b, ob, crit, x0, t0)        # kept alive across the capture below
+    assert lb0.grad_fn is not None
+    gs = GraphedTrainStep(b, crit, ob, (2, 1, 128, 128), (2, 128, 128))
+    for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(va, vb), ka
+    for x, t in batches[1:]:
+        la = _eager_step(a, oa, crit, x, t)
+        lb = gs(x, t)
+        torch.cuda.synchronize()
+        assert torch.equal(la.detach(), lb), (float(la), float(lb))
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa.grad, pb.grad)
+    for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(va, vb), ka
+    del la0, lb0
+
+
+def test_graphed_train_step_learning_rate():
+    """a float lr is frozen into the graph, so changing it raises; a device-tensor lr is read by the
+    fused step on every replay, so a scheduler's in-place update takes effect (eager-identical)."""
+    from unet.utils.graphed import GraphedTrainStep
+    from unet.utils.loss import DiceBCELoss
+    crit = DiceBCELoss()
+    batches = _batches(4)
+    # float lr: raises after a change
+    _, b = _twins(8)
+    ob = torch.optim.AdamW(b.parameters(), lr=1e-3, fused=True, capturable=True)
+    gs = GraphedTrainStep(b, crit, ob, (2, 1, 128, 128), (2, 128, 128))
+    gs(*batches[0])
+    ob.param_groups[0]["lr"] = 5e-4
+    with pytest.raises(RuntimeError, match="lr"):
+        gs(*batches[1])
+    # tensor lr driven by a scheduler, against the eager twin with the same scheduler
+    a, b = _twins(8)
+    mk = lambda m: torch.optim.AdamW(m.parameters(), lr=torch.tensor(1e-3, device="cuda"), weight_decay=1e-4,
+                                     fused=True, capturable=True)
+    oa, ob = mk(a), mk(b)
+    sa = torch.optim.lr_scheduler.StepLR(oa, step_size=1, gamma=0.5)
+    sb = torch.optim.lr_scheduler.StepLR(ob, step_size=1, gamma=0.5)
+    gs = GraphedTrainStep(b, crit, ob, (2, 1, 128, 128), (2, 128, 128))
+    for x, t in batches:
+        la = _eager_step(a, oa, crit, x, t)
+        lb = gs(x, t)
+        sa.step()
+        sb.step()
+        torch.cuda.synchronize()
+        assert torch.equal(la.detach(), lb), (float(la), float(lb))
+    assert float(ob.param_groups[0]["lr"]) == pytest.approx(1e-3 / 16)
+    for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(va, vb), ka

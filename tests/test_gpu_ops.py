@@ -508,7 +508,6 @@ Y_BENCH = [
 @pytest.mark.parametrize("stats", [True, False])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 def test_conv3_bench_tiles_y(prec, shape, stats, monkeypatch):
-    monkeypatch.setenv("UNET_CONV4", "0")   # the conv3 tiles (conv4 / conv5: test_gpu_conv4.py)
     monkeypatch.setenv("UNET_CONV5", "0")
     L = _lib()
     N, H, W, cin, cout, want = shape
@@ -554,7 +553,6 @@ DGRAD_BENCH = [
 @pytest.mark.parametrize("shape", DGRAD_BENCH, ids=lambda s: "x".join(map(str, s[:5])))
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 def test_conv3_bench_tiles_dgrad_f32(prec, shape, monkeypatch):
-    monkeypatch.setenv("UNET_CONV4", "0")   # the conv3 tiles (conv4 / conv5: test_gpu_conv4.py)
     monkeypatch.setenv("UNET_CONV5", "0")
     L = _lib()
     N, H, W, cin, cout, want = shape
@@ -581,7 +579,6 @@ def test_conv3_bench_tiles_dgrad_f32(prec, shape, monkeypatch):
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 def test_conv3_bench_tiles_dgrad_y(prec, shape, monkeypatch):
     """bf16 gradient of a DoubleConv's middle activation (the y epilogue without BN sums)."""
-    monkeypatch.setenv("UNET_CONV4", "0")   # the conv3 tiles (conv4 / conv5: test_gpu_conv4.py)
     monkeypatch.setenv("UNET_CONV5", "0")
     L = _lib()
     N, H, W, cin, cout = shape
@@ -718,7 +715,7 @@ def test_wgrad_source_kinds(prec, shape, kind):
     assert rel <= 2e-3, rel    # the gate / activation rounding to bf16 can differ by one ulp from torch's
 
 
-@pytest.mark.parametrize("path", ["conv5", "conv4", "conv3"])
+@pytest.mark.parametrize("path", ["conv5", "conv3"])
 @pytest.mark.parametrize("regime", ["centered", "offset"])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("shape", [(4, 256, 256, 64, 64), (4, 128, 128, 128, 128), (2, 64, 64, 256, 256),
@@ -732,7 +729,6 @@ def test_dgrad_y_bn_backward_sums(prec, shape, regime, path, monkeypatch):
     invstd·(Σg·y − mean·Σg) form cancels; its error must stay at fp32 summation-noise level relative to
     Σ|g·(y − mean)·invstd|."""
     monkeypatch.setenv("UNET_CONV5", "1" if path == "conv5" else "0")
-    monkeypatch.setenv("UNET_CONV4", "1" if path == "conv4" else "0")
     L, R = _lib(), _rt()
     N, H, W, cmid, cout = shape     # the conv cmid -> cout; its dgrad writes the cmid-channel gradient
     dt = DT[prec]

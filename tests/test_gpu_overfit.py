@@ -66,11 +66,11 @@ def test_overfit_c1_tumor_dice_vs_reference_spread():
     assert hip[-1][1] > 0.8 and r32[-1][1] > 0.8 and r64[-1][1] > 0.8
 
 
-@pytest.mark.skipif(__import__("os").environ.get("UNET_SLOW") != "1", reason="200-epoch run (~3 min); UNET_SLOW=1")
 def test_overfit_c1_full_protocol_final_dice():
-    """The reference's whole protocol (200 epochs, overfit_test.py:69): once converged the trajectories
-    meet again and the final Tumor-Dice agrees within 1e-3 (measured: HIP 0.999018, reference fp32
-    0.999214, fp64 0.998231; profiles/r02_overfit_c1_200ep.txt)."""
+    """The reference's whole protocol (200 epochs, overfit_test.py:69) and its statistic, the Tumor-Dice of the
+    last epoch (overfit_test.py:205,288): once converged the trajectories meet again and the final Tumor-Dice
+    agrees within the north_star's 1e-3 (round 2: HIP 0.999018, reference fp32 0.999214, fp64 0.998231;
+    profiles/r02_overfit_c1_200ep.txt).  Part of the default GPU suite since round 4."""
     D = _tools()
     from unet.models import AttentionUNet
     torch.backends.cudnn.deterministic = True
@@ -81,5 +81,8 @@ def test_overfit_c1_full_protocol_final_dice():
     x, t = D.batch(2, 512, 512)
     hip = D.run_hip(init, x, t, 200, 64)
     r32 = D.run_oracle(init, names, x, t, 200, torch.float32)
+    print("\nlast 10 epochs: dice_hip dice_ref32")
+    for i in range(190, 200):
+        print(i, "%.6f %.6f" % (hip[i][1], r32[i][1]))
     assert abs(hip[-1][1] - r32[-1][1]) <= 1e-3, (hip[-1], r32[-1])
     assert hip[-1][1] > 0.8

@@ -125,3 +125,16 @@ def test_metrics_compute_matches_reference_formulas(K):
         m = SegmentationMetrics(num_classes=K)
         m._cm = torch.from_numpy(cm.astype(np.int64))
         assert m.compute() == O.segmentation_scores(cm.astype(np.int64), m.class_names)
+
+
+def test_graphed_train_step_rejects_other_optimizers():
+    """GraphedTrainStep undoes its warm-up by restoring Adam's fresh state: any other optimizer, or a
+    non-capturable Adam, is refused before anything touches the device."""
+    from unet.models import UNet
+    from unet.utils.graphed import GraphedTrainStep
+    from unet.utils.loss import DiceBCELoss
+    m = UNet(1, 2, base_features=4)
+    with pytest.raises(RuntimeError, match="Adam"):
+        GraphedTrainStep(m, DiceBCELoss(), torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9), (1, 1, 8, 8), (1, 8, 8))
+    with pytest.raises(RuntimeError, match="capturable"):
+        GraphedTrainStep(m, DiceBCELoss(), torch.optim.AdamW(m.parameters(), lr=1e-3), (1, 1, 8, 8), (1, 8, 8))

@@ -1,9 +1,9 @@
-"""Ablation timing of conv4_kernel (csrc/conv4.hip, bf16 y mode) on full-size layers (diagnostic, GPU).
-Modes (bits): 1 no next-chunk halo staging; 2 no weight loads in the chunk loop; 4 no epilogue stores / sums;
-8 no per-chunk barrier; (--conv5: the LDS-DMA kernel, 16 no BN transform).  Times are medians of 10 launches; results are garbage for modes != 0."""
+"""Ablation timing of conv5_kernel (csrc/conv5.hip, bf16 y mode) on full-size layers (diagnostic, GPU).
+Modes (bits): 1 no in-loop halo DMA; 2 no in-loop weight DMA; 4 no epilogue stores / sums; 8 no per-chunk
+barrier; 16 no BN transform.  Times are medians of 10 launches; results are garbage for modes != 0."""
 import ctypes
 import os
-os.environ["UNET_CONV4"] = "1"   # conv4_eligible() is off by default
+os.environ["UNET_CONV5"] = "1"
 import statistics
 import sys
 from pathlib import Path
@@ -16,16 +16,10 @@ from unet._hip import lib as L  # noqa: E402
 from unet._hip.runtime import pack_weight, BF16, f32  # noqa: E402
 
 lib = L.load()
-lib.unet_diag_conv4_ablate.argtypes = [ctypes.POINTER(L.ConvDesc), ctypes.c_int, ctypes.c_void_p]
-lib.unet_diag_conv3_ablate.argtypes = [ctypes.POINTER(L.ConvDesc), ctypes.c_int, ctypes.c_void_p]
 lib.unet_diag_conv5_ablate.argtypes = [ctypes.POINTER(L.ConvDesc), ctypes.c_int, ctypes.c_void_p]
-C5 = "--conv5" in sys.argv
-if C5:
+if "--conv5" in sys.argv:     # accepted for older command lines
     sys.argv.remove("--conv5")
-    os.environ["UNET_CONV5"] = "1"
-else:
-    os.environ["UNET_CONV5"] = "0"
-FN = lib.unet_diag_conv5_ablate if C5 else lib.unet_diag_conv4_ablate
+FN = lib.unet_diag_conv5_ablate
 
 
 def layer(N, H, W, cin, cout, kind):
@@ -53,7 +47,7 @@ def layer(N, H, W, cin, cout, kind):
 
 
 def main():
-    modes = [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3,4,8,7,15").split(",")]
+    modes = [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3,4,8,7,15,16,31").split(",")]
     for (N, H, W, cin, cout, kind) in [(4, 512, 512, 64, 64, L.SRC_ACT), (4, 512, 512, 64, 64, L.SRC_PLAIN),
                                        (4, 256, 256, 128, 128, L.SRC_ACT), (4, 128, 128, 256, 256, L.SRC_PLAIN)]:
         d, keep = layer(N, H, W, cin, cout, kind)

@@ -1,0 +1,61 @@
+#!/bin/bash
+# Round-4 GPU evidence, one parameterised script (replaces round 3's one-off gpu_r03*.sh files).
+#   TAG=<dir under gpurun_out>  STEPS="tests smoke bench c5 c2 trace layerprof pmc hbmpmc sq repro"  bash tools/gpu_r04.sh
+# Every GPU step runs under its own time limit; the chain stops at the first failure (no retries).
+set -o pipefail
+O=gpurun_out/${TAG:-r04}
+mkdir -p $O
+export TMPDIR=/tmp
+fail() { echo "$1 failed"; tail -${3:-30} "$2"; exit 1; }
+for step in ${STEPS:-tests smoke bench}; do
+  case $step in
+  tests)   # the driver's -m gpu suite, with per-test durations
+    timeout -k 10 ${TLIM:-1100} python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread --durations=40 ${PYARGS} > $O/gpu_tests.log 2>&1 \
+      || { grep -E "FAILED|Error|passed|failed" $O/gpu_tests.log | tail -20; fail tests $O/gpu_tests.log 60; }
+    grep -E "passed|failed" $O/gpu_tests.log | tail -2 ;;
+  some)    # a subset: PYARGS selects
+    timeout -k 10 ${TLIM:-900} python -u -m pytest -m gpu -x -v --timeout 400 --timeout-method thread --durations=20 ${PYARGS} > $O/some_tests.log 2>&1 \
+      || fail some $O/some_tests.log 60
+    grep -E "passed|failed" $O/some_tests.log | tail -2 ;;
+  smoke)
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+    tail -1 $O/smoke.log ;;
+  bench)   # the driver's default bench line
+    timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || fail bench $O/bench.err
+    cat $O/bench.json ;;
+  benchq)  # a quick headline-only line
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-fp32-line --no-graph-line ${BARGS} > $O/benchq.json 2> $O/benchq.err || fail benchq $O/benchq.err
+    cat $O/benchq.json ;;
+  c5)
+    timeout -k 10 300 python -u bench.py --precision fp16 --in-ch 3 --size 1024 --accum 8 --steps 5 --warmup 2 --no-cpu-baseline --no-fp32-line > $O/bench_c5.json 2> $O/bench_c5.err || fail c5 $O/bench_c5.err
+    cat $O/bench_c5.json ;;
+  c2)
+    timeout -k 10 300 python -u bench.py --model unet --no-cpu-baseline --no-fp32-line --no-graph-line > $O/bench_c2.json 2> $O/bench_c2.err || fail c2 $O/bench_c2.err
+    cat $O/bench_c2.json ;;
+  trace)   # kernel-trace stats of the bench command
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-fp32-line --no-graph-line > $O/trace.log 2>&1 || fail trace $O/trace.log
+    python tools/profsum.py $O/trace > $O/trace_summary.txt 2>&1; head -40 $O/trace_summary.txt ;;
+  layerprof)
+    timeout -k 10 300 python -u tools/layerprof.py > $O/layerprof.txt 2>&1 || fail layerprof $O/layerprof.txt
+    tail -5 $O/layerprof.txt ;;
+  pmc)     # HBM bytes of the conv family and of the HBM-bound kernels (FETCH_SIZE and WRITE_SIZE in separate passes)
+    i=0
+    for set in FETCH_SIZE WRITE_SIZE; do
+      i=$((i+1))
+      timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $O/pmc$i -o pmc -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-fp32-line --no-graph-line > $O/pmc$i.log 2>&1 || fail "pmc pass $i" $O/pmc$i.log 5
+    done
+    python tools/traffic.py --all $O/pmc1 $O/pmc2 > $O/traffic.log 2>&1 || fail traffic $O/traffic.log
+    tail -40 $O/traffic.log ;;
+  sq)      # instruction mix of the conv5 / wgrad5 kernels (SQ counters, one pass)
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_BRANCH --kernel-include-regex "${SQRE:-conv5_kernel|wgrad5_kernel}" --output-format csv -d $O/sq -o sq -- python tools/layerprof.py > $O/sq.log 2>&1 || fail sq $O/sq.log 5
+    python tools/pmcsum.py $O/sq "${SQRE:-conv5_kernel|wgrad5_kernel}" > $O/sq_summary.txt 2>&1; cat $O/sq_summary.txt | head -40 ;;
+  ablate)
+    timeout -k 10 300 python -u tools/conv5_ablate.py ${ABL:-0,4,16,31} > $O/conv5_ablate.txt 2>&1 || fail ablate $O/conv5_ablate.txt
+    cat $O/conv5_ablate.txt ;;
+  repro)   # round 3's GraphedTrainStep crash (old capture path); last in a call: it may end in a segfault
+    PYTHONFAULTHANDLER=1 timeout -k 10 180 python -u tools/repro_graphed_live_graph.py ${REPRO:-backward} > $O/repro.log 2>&1; echo "repro rc $?" >> $O/repro.log
+    tail -40 $O/repro.log ;;
+  *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo done

@@ -20,7 +20,6 @@
 namespace unet {
 
 constexpr int CTW = 16;          // tile width in pixels
-constexpr int PACK_NPAD = 128;   // packed rows padded to the largest BN
 
 // ------------------------------------------------------------------------------------------------
 // epilogue shared by conv2 / conv3.  acc[i][j][r] (lane l): pixel (h0 + MI*wm + i, w0 + 4*(l>>4) + r),
@@ -489,10 +488,6 @@ int pack_tiles_launch(int dtype, int count, const unet_pack_job* jobs, hipStream
 int conv5_run(const unet_conv_desc* d, hipStream_t st);
 int conv5_stats_rows(const unet_conv_desc* d);
 int conv5_variant(const unet_conv_desc* d, char* buf, int len);
-bool conv4_eligible(const unet_conv_desc* d);   // conv4.hip: the 32x32x16-MFMA 3x3 path
-int conv4_run(const unet_conv_desc* d, hipStream_t st);
-int conv4_stats_rows(const unet_conv_desc* d);
-int conv4_variant(const unet_conv_desc* d, char* buf, int len);
 bool smallcin_conv_ok(const unet_conv_desc* d);  // smallcin.hip
 bool pw_conv_ok(const unet_conv_desc* d);        // pw.hip
 int pw_conv_rows(const unet_conv_desc* d);
@@ -521,7 +516,6 @@ static int dispatch_conv(const unet_conv_desc* d, hipStream_t st) {
   if (!fast_eligible(d)) return dispatch_generic<T>(d, st);
   if constexpr (sizeof(T) == 2) {
     if (conv5_eligible(d)) return conv5_run(d, st);
-    if (conv4_eligible(d)) return conv4_run(d, st);
   }
   const ConvCfg c = pick_cfg(d);
   if constexpr (sizeof(T) == 2) {
@@ -609,7 +603,7 @@ int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8)
 // does unet_conv reduce d's bnb_* sums in the conv epilogue (rows = the conv's M tiles)?
 static bool bnb_in_epilogue(const unet_conv_desc* d) {
   if (smallcin_conv_ok(d) || pw_conv_ok(d) || !fast_eligible(d) || d->dtype == UNET_F32) return false;
-  if (conv5_eligible(d) || conv4_eligible(d)) return true;
+  if (conv5_eligible(d)) return true;
   return conv3_bnb_tile(d, pick_cfg(d));
 }
 
@@ -619,7 +613,6 @@ int unet_conv_stats_rows(const unet_conv_desc* d) {
   if (pw_conv_ok(d)) return pw_conv_rows(d);
   if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
   if (conv5_eligible(d)) return conv5_stats_rows(d);
-  if (conv4_eligible(d)) return conv4_stats_rows(d);
   const ConvCfg c = pick_cfg(d);
   return d->N * cdiv(d->W, CTW) * cdiv(d->H, 4 * c.wm);
 }
@@ -638,7 +631,6 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
     return 0;
   }
   if (conv5_eligible(d)) return conv5_variant(d, buf, len);
-  if (conv4_eligible(d)) return conv4_variant(d, buf, len);
   const ConvCfg c = pick_cfg(d);
   if (conv3_eligible(d)) {
     // the (wm, wn, ntn) block tile of pick_cfg; 16-row tiles run as MI=8 waves (dispatch_conv3)

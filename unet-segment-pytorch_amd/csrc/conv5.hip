@@ -3,8 +3,8 @@
 // Replaces nn.Conv2d(k=3, pad=1, bias=False) of unet/models/layers.py:32,35 (every DoubleConv half) and the
 // input-gradient half of its convolution_backward, on maps large enough to fill the chip.
 //
-// Why: the register-staged kernels (conv3, conv4) spend most of their time waiting, not computing.  The
-// conv4 ablations (tools/conv4_ablate.py, 64->64 @ 4x512^2): 142 us full; 54 us with the halo staging, the
+// Why: register-staged kernels spend most of their time waiting, not computing.  The round-3 ablations of a
+// register-staged 32x32x16 kernel (since removed; 64->64 @ 4x512^2): 142 us full; 54 us with the halo staging, the
 // in-loop weight loads and the epilogue removed, i.e. the MFMA + LDS loop alone runs at 57 % of the bf16 peak.
 // The halo staging cost 39 us: its loads were issued 6 taps (~0.6 us) before use, less than the load
 // latency under full-chip streaming, and held registers while in flight.  Here every operand reaches LDS by
@@ -27,7 +27,7 @@
 //
 // Tile: 16 rows x 32 px x 64 output channels per workgroup of 8 waves (4 row groups x 2 channel halves);
 // wave tile MI=4 rows x 32 px x 32 channels on v_mfma_f32_32x32x16 (D[co][px] = W[co][k] X[k][px]),
-// persistent over M tiles.  Epilogues as conv4: y (16-bit) + BatchNorm partial sums, y + BatchNorm-backward
+// persistent over M tiles.  Epilogues: y (16-bit) + BatchNorm partial sums, y + BatchNorm-backward
 // sums (bnb_*), fp32 gradient (split / accumulate); the sums are per lane across the workgroup's tiles and
 // reduced once (one partial row per wave row group: [.. gridDim.x * 4 ..]).
 #include "conv_mfma32.h"
@@ -39,7 +39,7 @@ constexpr int C5_W = 32, C5_HW = 34;     // tile width, halo width (pixels)
 constexpr int C5_WM = 4, C5_WN = 2, C5_NW = 8, C5_NT = 512;
 constexpr int C5_BN = 64;                // output channels per workgroup
 constexpr int C5_CMAX = 1024;            // largest BN-activation source (scale / shift table)
-constexpr int C5_NPAD = 128;             // packed weight rows are padded to this (conv.hip PACK_NPAD)
+constexpr int C5_NPAD = PACK_NPAD;       // packed weight rows are padded to this (conv_common.h)
 constexpr int OM5_Y = 0, OM5_F32 = 1, OM5_BNB = 2;
 
 template <int MI, bool ACT>
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   }
   lds_barrier();
 
-  // BatchNorm sums of this lane's pixel column over the block's tiles (see conv4.hip)
+  // BatchNorm sums of this lane's pixel column over the block's tiles (reduced once, after the last tile)
   constexpr bool SUMS = OM == OM5_Y || OM == OM5_BNB;
   float sA[16], sB[16];
 #pragma unroll
@@ -740,7 +740,7 @@ static int abl5(const unet_conv_desc* d, int abl, hipStream_t st) {
 }  // namespace unet
 
 // diagnostic (not part of the C ABI header): conv5 ablations of the bf16 y-mode kernel (ABL bits above) on a
-// one-source plain or BN-activation descriptor; tools/conv4_ablate.py --conv5
+// one-source plain or BN-activation descriptor; tools/conv5_ablate.py
 extern "C" int unet_diag_conv5_ablate(const unet_conv_desc* d, int abl, void* stream) {
   using namespace unet;
   if (!conv5_eligible(d) || d->nsrc != 1 || d->out_mode != UNET_OUT_Y || d->dtype != UNET_BF16) return UNET_ERR_ARG;

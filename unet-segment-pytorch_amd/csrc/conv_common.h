@@ -46,6 +46,10 @@ __device__ __forceinline__ void store_shuffle2(const unet_conv_desc& d, long lon
   reinterpret_cast<T*>(d.out)[o] = from_f<T>(v + (d.bias ? d.bias[c] : 0.f));
 }
 
+// packed weight rows (Cout, or Cin for the transposed dgrad weights) are padded to this: the largest
+// output-channel block of any conv kernel (unet_packed_weight_elems, pack.hip, conv5.hip)
+constexpr int PACK_NPAD = 128;
+
 template <typename T> __host__ __device__ constexpr int kc_of() { return sizeof(T) == 2 ? 32 : 16; }
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 __device__ __forceinline__ int round_up_d(int a, int b) { return (a + b - 1) / b * b; }

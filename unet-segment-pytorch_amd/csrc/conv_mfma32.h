@@ -1,4 +1,4 @@
-// conv_mfma32.h — the 32x32x16 MFMA operand traits and half-wave reductions shared by conv4.hip / conv5.hip.
+// conv_mfma32.h — the 32x32x16 MFMA operand traits and half-wave reductions used by conv5.hip.
 #pragma once
 #include "conv_src16.h"
 

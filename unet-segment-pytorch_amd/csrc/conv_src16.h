@@ -1,5 +1,5 @@
 // conv_src16.h — the 16-bit conv kernels' halo staging: buffer-resource loads of virtual activations
-// (conv3_body.inc, conv4.hip).  One 16-byte channel vector of one halo pixel per staged item:
+// (conv3_body.inc).  One 16-byte channel vector of one halo pixel per staged item:
 //  * every global read is a buffer load (SGPR descriptor + 32-bit offset).  Zero padding, pixels
 //    outside the placed up-sampled map and channels past the source all read as 0 through the
 //    descriptor's range check (offset >= OOB), so no load sits behind a per-lane branch;

@@ -78,7 +78,7 @@ int pack_tiles_launch(int dtype, int count, const unet_pack_job* jobs, hipStream
     pt.j[i] = jobs[i];
     pt.tile0[i] = tot;
     const int rows = jobs[i].transpose ? jobs[i].Cin : jobs[i].Cout, cols = jobs[i].transpose ? jobs[i].Cout : jobs[i].Cin;
-    const int rows_pad = (rows + 127) / 128 * 128;
+    const int rows_pad = round_up(rows, PACK_NPAD);   // = packed_rows() of unet_packed_weight_elems
     tot += rows_pad / 16 * ((cols + 31) / 32);
   }
   pt.tile0[count] = tot;

@@ -17,7 +17,8 @@ from torch.autograd.function import once_differentiable
 from . import lib as L
 from .runtime import (Act, act_from_nchw, act_to_nchw, f32, get_precision, grad_nchw_to_nhwc, grad_nhwc_to_nchw,
                       nchw_src, require_device, stream, up_scale, vp)
-from .stages import (DoubleConvStage, DownStage, GateStage, Grads, NetworkPlan, OutConvStage, UpStage)
+from .stages import (DoubleConvStage, DownStage, GateStage, Grads, NetworkPlan, OutConvStage, UpStage,
+                     mark_tracked)
 
 
 # the plan's activation-gradient buffers and packed dgrad weights are consumed by the first backward
@@ -52,6 +53,7 @@ def _apply(plan, module: torch.nn.Module, inputs: List[torch.Tensor]):
     params = [p for p in module.parameters()]
     track = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or any(i.requires_grad for i in inputs))
     if not track:
+        plan.tracked = False
         return plan.forward(inputs, [False] * len(inputs))
     return list(_PlanFn.apply(plan, params, len(inputs), *inputs, *params))
 
@@ -159,6 +161,11 @@ class _ModulePlan:
         self.kind = kind
         self.prec = get_precision(module)
         self.training = module.training
+        self.tracked = True      # False: no backward follows (set by _apply)
+
+    def _stage(self, st):
+        mark_tracked(st, self.tracked)
+        return st
 
     def forward(self, inputs, needs):
         prec, tr = self.prec, self.training
@@ -169,24 +176,24 @@ class _ModulePlan:
         if k == "double_conv":
             x = xs[0]
             N, C, H, W = x.shape
-            self.st = DoubleConvStage(self.m)
+            self.st = self._stage(DoubleConvStage(self.m))
             self.out = self.st.forward(prec, [nchw_src(x)], N, H, W, tr, keep=x)
             return [act_to_nchw(self.out, prec)]
         self.acts = [act_from_nchw(x, prec) for x in xs]
         if k == "down":
-            self.st = DownStage(self.m)
+            self.st = self._stage(DownStage(self.m))
             self.out = self.st.forward(prec, self.acts[0], tr)
             return [act_to_nchw(self.out, prec)]
         if k in ("up", "attention_up"):
-            self.st = UpStage(self.m, k == "attention_up")
+            self.st = self._stage(UpStage(self.m, k == "attention_up"))
             self.out = self.st.forward(prec, self.acts[0], self.acts[1], tr)
             return [act_to_nchw(self.out, prec)]
         if k == "out_conv":
-            self.st = OutConvStage(self.m)
+            self.st = self._stage(OutConvStage(self.m))
             return [self.st.forward(prec, self.acts[0])]
         if k == "attention_gate":
             g, x = self.acts
-            self.st = GateStage(self.m)
+            self.st = self._stage(GateStage(self.m))
             self.st.forward(prec, g, x, tr)
             out = f32(x.N, x.C, x.H, x.W, device=x.data.device)
             L.call("unet_gated_to_nchw", prec.code, x.N, x.C, x.H, x.W, vp(x.data), vp(x.ab[0]), vp(x.ab[1]),

@@ -71,6 +71,7 @@ class ConvBN:
         self.pre_wt = None
         self.wsrcs = None    # weight-gradient sources when the forward stored its transformed input
         self.wact = None
+        self.tracked = True  # a backward will follow this forward (act_out only pays off then)
 
     # ---- forward ----
     def forward(self, prec: Precision, srcs: List[L.Src], N: int, H: int, W: int, training: bool,
@@ -88,7 +89,7 @@ class ConvBN:
         # y), and the extra 2-byte-per-element write cost as much there (+50 us) as the wgrad saves
         # (profiles/r03_layerprof_act_out.txt)
         self.wsrcs = self.wact = None
-        if training and srcs[0].kind == L.SRC_ACT and H * W <= 256 * 256 and not os.environ.get("UNET_NO_ACT_OUT") \
+        if training and self.tracked and srcs[0].kind == L.SRC_ACT and H * W <= 256 * 256 and not os.environ.get("UNET_NO_ACT_OUT") \
                 and L.load().unet_conv_act_out_ok(d):
             act = torch.empty(N, H, W, srcs[0].C, dtype=prec.torch_dtype, device=dev)
             d.act_out = act.data_ptr()
@@ -440,6 +441,18 @@ class GateStage:
 
 
 # ------------------------------------------------------------------------------------------------
+def mark_tracked(stage, tracked: bool):
+    """Tell every ConvBN of a stage whether a backward will follow its forward."""
+    for attr in ("c1", "c2", "cg", "cx"):
+        cb = getattr(stage, attr, None)
+        if cb is not None:
+            cb.tracked = tracked
+    for attr in ("dc", "gate"):
+        sub = getattr(stage, attr, None)
+        if sub is not None:
+            mark_tracked(sub, tracked)
+
+
 def _pad_geometry(x1: Act, x2: Act):
     up_h, up_w = 2 * x1.H, 2 * x1.W
     dy, dx = x2.H - up_h, x2.W - up_w
@@ -750,6 +763,7 @@ class NetworkPlan:
         cbs = self.convbns()
         for cb, wp in zip(cbs, pack_many([(cb.conv.weight, False) for cb in cbs], prec)):
             cb.pre_wp = wp
+            cb.tracked = tracked
         self.xs, self.dec = [], []
 
     def fwd_inc(self):

@@ -1,16 +1,34 @@
 """A training micro-step captured into a HIP graph (opt-in; reference loop: scripts/train.py:127-143).
 
-The eager step costs ~300 C-ABI calls plus the torch allocator and autograd bookkeeping on the host
+The eager step costs ~260 C-ABI calls plus the torch allocator and autograd bookkeeping on the host
 (tools/cpu_overhead.py).  `GraphedTrainStep` captures forward -> loss -> backward -> clip_grad_norm_ ->
 optimizer.step for one fixed batch shape into a hipGraph (torch.cuda.CUDAGraph drives it on ROCm) and
 replays it per batch, so the host enqueues one graph launch per step and the GPU runs the identical
-kernels.  Requirements, as for any whole-step graph capture in PyTorch: a fixed input / target shape, a
-capturable optimizer (`capturable=True`, e.g. AdamW(fused=True, capturable=True)) whose fresh state is
-all zeros (Adam / AdamW: the warm-up steps before capture are undone by restoring the weights and buffers
-and zeroing the optimizer state they created), no loss scaler (its step reads the inf flag on the host)
-and no DistributedDataParallel (its reducer is not captured here).
+kernels.
+
+Requirements, checked in __init__ (RuntimeError otherwise): a fixed input / target shape; a torch.optim.Adam
+or AdamW with `capturable=True` in every parameter group (their fresh state is all zeros, which is what
+undoing the warm-up restores); no loss scaler (its step reads the inf flag on the host) and no
+DistributedDataParallel (its reducer is not captured here).
+
+Hyperparameters: a replay runs the optimizer step exactly as captured.  A python-float hyperparameter
+(lr, weight_decay, betas, eps, ...) is therefore frozen into the graph, and __call__ raises RuntimeError if
+one has changed since capture instead of silently training with the old value.  To drive the learning rate
+with a scheduler (scripts/train.py:353-370), give the optimizer a device tensor lr
+(`AdamW(..., lr=torch.tensor(1e-3, device="cuda"), capturable=True)`): the fused step reads it from device
+memory on every replay, and torch's LR schedulers update a tensor lr in place.
+
+Gradients: the backward is taken with torch.autograd.grad over the parameters (no AccumulateGrad nodes
+run), and the results are assigned to `p.grad`.  That matters when the caller still holds an eager step's
+autograd graph (e.g. its `loss`): its AccumulateGrad nodes were created on the default stream, stay
+attached to the parameters while that graph lives, and a `.backward()` inside the capture would route the
+gradient of every parameter through them — a cross-stream wait on the default stream in the middle of a
+stream capture ("GraphedTrainStep and a live eager graph").  Values are identical: every
+parameter gets exactly one gradient per step, which AccumulateGrad would only have stored.
+
 Weights, BN running statistics and optimizer state live in their own tensors and are updated in place by
-every replay; `loss` is a device tensor that every replay overwrites.
+every replay; `loss` is a device tensor that every replay overwrites; `p.grad` are the step's gradients
+(graph-owned memory, overwritten by every replay).
 """
 
 from __future__ import annotations
@@ -20,10 +38,20 @@ from typing import Callable, Optional, Sequence
 import torch
 
 
+def _frozen_hyperparameters(optimizer: torch.optim.Optimizer):
+    """Per parameter group: every non-tensor hyperparameter (a graph replay uses the value captured)."""
+    return [{k: v for k, v in g.items() if k != "params" and not torch.is_tensor(v)} for g in optimizer.param_groups]
+
+
 class GraphedTrainStep:
     def __init__(self, model: torch.nn.Module, criterion: Callable, optimizer: torch.optim.Optimizer,
                  input_shape: Sequence[int], target_shape: Sequence[int], target_dtype=torch.int64,
                  clip_norm: Optional[float] = 1.0, warmup: int = 3, device="cuda"):
+        if not isinstance(optimizer, (torch.optim.Adam, torch.optim.AdamW)):
+            raise RuntimeError(f"GraphedTrainStep: needs torch.optim.Adam / AdamW (capturable=True), got "
+                               f"{type(optimizer).__name__}: undoing the warm-up steps restores Adam's fresh state")
+        if not all(g.get("capturable", False) for g in optimizer.param_groups):
+            raise RuntimeError("GraphedTrainStep: the optimizer must be built with capturable=True")
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.clip_norm = clip_norm
@@ -41,9 +69,11 @@ class GraphedTrainStep:
         torch.cuda.current_stream(device).wait_stream(s)
         self._restore(snap)
         self.optimizer.zero_grad(set_to_none=True)
+        self.hyper = _frozen_hyperparameters(optimizer)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.loss = self._body()
+        self.grads = [p.grad for p in self.params]
 
     def _state_tensors(self):
         return [v for st in self.optimizer.state.values() for v in st.values() if torch.is_tensor(v)]
@@ -66,7 +96,10 @@ class GraphedTrainStep:
 
     def _body(self) -> torch.Tensor:
         loss = self.criterion(self.model(self.x), self.t)
-        loss.backward()
+        # autograd.grad, not backward(): no AccumulateGrad node runs (see the module docstring)
+        grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        for p, g in zip(self.params, grads):
+            p.grad = g
         if self.clip_norm is not None:
             torch.nn.utils.clip_grad_norm_(self.params, self.clip_norm)
         self.optimizer.step()
@@ -74,7 +107,17 @@ class GraphedTrainStep:
 
     def __call__(self, x: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
         """One step on (x, t); returns the step's loss (a device tensor overwritten by the next call)."""
+        # the keys captured (a scheduler built later adds its own bookkeeping keys, e.g. initial_lr)
+        diff = sorted({k for g, cap in zip(self.optimizer.param_groups, self.hyper) for k, v in cap.items()
+                       if torch.is_tensor(g.get(k)) or g.get(k) != v})
+        if diff or len(self.optimizer.param_groups) != len(self.hyper):
+            raise RuntimeError(
+                f"GraphedTrainStep: optimizer hyperparameter(s) {diff} changed since capture; a graph replay runs "
+                "the captured values.  Pass lr as a device tensor (lr=torch.tensor(v, device='cuda')) so a "
+                "scheduler updates it in place, or build a new GraphedTrainStep.")
         self.x.copy_(x, non_blocking=True)
         self.t.copy_(t, non_blocking=True)
         self.graph.replay()
+        for p, g in zip(self.params, self.grads):
+            p.grad = g
         return self.loss
