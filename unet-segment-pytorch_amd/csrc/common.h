@@ -112,35 +112,23 @@ __device__ __forceinline__ void unpack8_16(const uint4& q, float* v) {
     for (int i = 0; i < 8; ++i) v[i] = (float)h[i];
   }
 }
+// two floats -> one dword of two 16-bit values, round to nearest even: __builtin_convertvector on a float2 is
+// one v_cvt_pk_{bf16,f16}_f32 (two scalar conversions compiled to two converts and a v_perm)
 template <typename T>
-__device__ __forceinline__ uint4 pack8_16(const float* v) {
+__device__ __forceinline__ unsigned pack2_16(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) float f32x2;
   if constexpr (__is_same(T, bf16)) {
     typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-    unsigned u[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16x2 p = {(__bf16)v[2 * i], (__bf16)v[2 * i + 1]};
-      u[i] = __builtin_bit_cast(unsigned, p);
-    }
-    return make_uint4(u[0], u[1], u[2], u[3]);
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{a, b}), bf16x2));
   } else {
-    f16x8 h;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) h[i] = (f16)v[i];
-    return __builtin_bit_cast(uint4, h);
+    typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2{a, b}), f16x2));
   }
 }
 template <typename T>
-__device__ __forceinline__ unsigned pack2_16(float a, float b) {
-  if constexpr (__is_same(T, bf16)) {
-    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-    const bf16x2 p = {(__bf16)a, (__bf16)b};
-    return __builtin_bit_cast(unsigned, p);
-  } else {
-    typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
-    const f16x2 p = {(f16)a, (f16)b};
-    return __builtin_bit_cast(unsigned, p);
-  }
+__device__ __forceinline__ uint4 pack8_16(const float* v) {
+  return make_uint4(pack2_16<T>(v[0], v[1]), pack2_16<T>(v[2], v[3]), pack2_16<T>(v[4], v[5]),
+                    pack2_16<T>(v[6], v[7]));
 }
 
 // run `body` with T = float / bf16 / f16 for a UNET_F32 / UNET_BF16 / UNET_F16 code

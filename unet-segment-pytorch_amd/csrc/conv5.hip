@@ -64,11 +64,12 @@ struct C5Layout {
   static constexpr int BYTES = OFF_JUNK + 1024;
 };
 
-// wave tile: MI rows x 32 px x 32 channels; SK: SK_PLAIN (every source stored as is) or SK_ACT / SK_ACT_PLAIN
-// (src0 a BN activation, optionally gated; src1 stored).  ABL (diagnostic ablations, unet_diag_conv5_ablate;
-// 0 in the product): 1 no in-loop halo DMA, 2 no in-loop weight DMA, 4 no epilogue, 8 no per-chunk barrier,
-// 16 no BN transform
-template <typename T, int MI, int OM, int SK, int ABL = 0>
+// wave tile: MI rows x 32 px x 32 channels; SK: SK_PLAIN (every source stored as is), SK_ACT (one source, a BN
+// activation) or SK_ACT_PLAIN (src0 a BN activation, src1 — if any — stored); GATE: src0 carries the attention
+// gate (compile-time, so the transform is one straight-line block).  ABL (diagnostic ablations,
+// unet_diag_conv5_ablate; 0 in the product): 1 no in-loop halo DMA, 2 no in-loop weight DMA, 4 no epilogue,
+// 8 no per-chunk barrier, 16 no BN transform
+template <typename T, int MI, int OM, int SK, int GATE, int ABL = 0, int PIPE = 1>
 __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d, int tiles_w, int tiles_h, int mtiles,
                                                         int nch) {
   using F = typename Mma32<T>::frag;
@@ -99,7 +100,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   const long long npix = (long long)d.N * d.H * d.W;
   const rsrc4_t rs0 = mk_rsrc4(s0.data, (unsigned)(npix * C0 * 2));
   const rsrc4_t rs1 = d.nsrc > 1 ? mk_rsrc4(s1.data, (unsigned)(npix * s1.C * 2)) : rs0;
-  const bool gated = ACT && s0.gate_p != nullptr;
+  constexpr bool gated = ACT && GATE;
   const rsrc4_t rsg = mk_rsrc4(gated ? (const void*)s0.gate_p : s0.data, (unsigned)(npix * 4));
   float ga = 0.f, gb = 0.f;
   if (gated) { ga = s0.gate_ab[0]; gb = s0.gate_ab[1]; }
@@ -170,24 +171,42 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     }
   };
 
+  // Per-tile slot offsets, recomputed at a tile's first chunk (a wave-uniform branch), so that a chunk's DMA
+  // and transform cost one add per slot: ib0 / ib1 = byte offset of the slot's pixel in src0 / src1 plus its
+  // channel half (>= OOB for zero-padding pixels and slots past the image); xok / xao for the transform
+  // cursor: the slot's pixel inside the image / its act_out byte offset (interior pixels only, else >= OOB)
+  unsigned ib0[DPW], ib1[DPW], xao[DPW];
+  bool xok[DPW];
+  auto tile_slots = [&](const Cur& q, unsigned (&o0)[DPW], unsigned (&o1)[DPW]) {
+    const unsigned pbase = ((unsigned)q.n * d.H + q.h0) * d.W + q.w0;
+#pragma unroll
+    for (int k = 0; k < DPW; ++k) {
+      const int y = q.h0 + soy[k], x = q.w0 + sox[k];
+      const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
+      const unsigned pix = pbase + (unsigned)(soy[k] * d.W + sox[k]);
+      o0[k] = ok ? (pix * (unsigned)C0 + 8u * hbit[k]) * 2u : OOB;
+      o1[k] = ok ? (pix * (unsigned)(d.nsrc > 1 ? s1.C : C0) + 8u * hbit[k]) * 2u : OOB;
+    }
+  };
+
   // DMA of the chunk at cursor q: halo slots, weight fragments, and at a gated tile's first chunk the gate
   // pre-activations of this lane's slots (returns whether those went out: the chunk counts ND + DPW)
   auto issue = [&](const Cur& q, bool prologue) -> bool {
+    if (q.c == 0) tile_slots(q, ib0, ib1);
     const int cn0 = q.c * 16;
     const bool s1sel = d.nsrc > 1 && cn0 >= C0;
     const int cl = s1sel ? cn0 - C0 : cn0;
     const int Cs = s1sel ? s1.C : C0;
+    const bool rag = cl + 16 > Cs;                  // the chunk's upper channel half is past the source
     const rsrc4_t rs = s1sel ? rs1 : rs0;
     const unsigned img = l32 + (ACT ? Lay::OFF_RAW + q.s2 * Lay::IMG : Lay::OFF_COMP + q.s3 * Lay::IMG);
-    const unsigned pbase = ((unsigned)q.n * d.H + q.h0) * d.W + q.w0;
     if (!(ABL & 1) || prologue) {
 #pragma unroll
       for (int k = 0; k < DPW; ++k) {
         const int i = wave + k * C5_NW;
-        const int y = q.h0 + soy[k], x = q.w0 + sox[k], ch = cl + 8 * hbit[k];
-        const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W) & (ch < Cs);
-        const unsigned pix = pbase + (unsigned)(soy[k] * d.W + sox[k]);
-        dma16(rs, i < NI ? img + i * 1024 : junk, ok ? (pix * (unsigned)Cs + (unsigned)ch) * 2u : OOB);
+        unsigned vo = (s1sel ? ib1[k] : ib0[k]) + (unsigned)cl * 2u;   // stays >= OOB when the base is
+        if (rag && hbit[k]) vo = OOB;
+        dma16(rs, i < NI ? img + i * 1024 : junk, vo);
       }
     }
     if (!(ABL & 2) || prologue) {
@@ -205,77 +224,94 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     const bool gl = gated && q.c == 0;
     if (gl) {
       const unsigned gd = l32 + Lay::OFF_GATE + (q.ti & 1) * Lay::GATE;
+      const unsigned pbase = ((unsigned)q.n * d.H + q.h0) * d.W + q.w0;
 #pragma unroll
       for (int k = 0; k < DPW; ++k) {
         const int i = wave + k * C5_NW;
-        const int y = q.h0 + soy[k], x = q.w0 + sox[k];
-        const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
         const unsigned pix = pbase + (unsigned)(soy[k] * d.W + sox[k]);
-        dma4(rsg, i < NI ? gd + i * 256 : junk, ok ? pix * 4u : OOB);
+        dma4(rsg, i < NI ? gd + i * 256 : junk, ib0[k] < OOB ? pix * 4u : OOB);
       }
     }
     return gl;
   };
 
   // BN-activation (+gate) transform of the chunk at cursor q, raw -> compute image, this lane's own slots
-  // (zero-padding pixels and the image's tail slots come out 0)
+  // (zero-padding pixels and the image's tail slots come out 0).  Two channels per VALU op: v_pk_fma_f32 for
+  // the affine (fp32, as before: the same roundings), the gate / zero-padding multiply as v_pk_mul_f32, and
+  // ReLU after the 16-bit rounding as v_pk_max_i16 against 0 (a 16-bit float is negative iff its sign bit is
+  // set; rounding is monotone and maps 0 to 0, and the multiplier is >= 0, so max(round(t*g), 0) equals
+  // round(max(t, 0)*g) — the same bits up to the sign of zero)
   T* const aout = (ACT && OM == OM5_Y && blockIdx.y == 0) ? (T*)d.act_out : nullptr;
-  const rsrc_t rao = mk_rsrc(aout ? (const void*)aout : d.out, (unsigned)(npix * C0 * 2));
+  const rsrc_t rao = mk_rsrc(aout ? (const void*)aout : d.out, (unsigned)(aout ? npix * C0 * 2 : 0));
   bool ns_prev = false;   // the last transform issued DPW act_out stores (after the DMA batch the next wait needs)
+  typedef __attribute__((ext_vector_type(2))) float f2_t;
+  typedef __attribute__((ext_vector_type(2))) short s2_t;
+  const s2_t lo2 = s0.relu ? s2_t{0, 0} : s2_t{-32768, -32768};   // ReLU as a 16-bit integer max (no-op: -32768)
   auto transform = [&](const Cur& q) {
+    if (q.c == 0) {
+      const unsigned pbase = ((unsigned)q.n * d.H + q.h0) * d.W + q.w0;
+#pragma unroll
+      for (int k = 0; k < DPW; ++k) {
+        const int y = q.h0 + soy[k], x = q.w0 + sox[k];
+        xok[k] = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
+        const bool in = xok[k] && (unsigned)soy[k] < (unsigned)TH && (unsigned)sox[k] < (unsigned)C5_W;
+        const unsigned pix = pbase + (unsigned)(soy[k] * d.W + sox[k]);
+        xao[k] = in ? (pix * (unsigned)C0 + 8u * hbit[k]) * 2u : OOB;
+      }
+    }
     const int cn0 = q.c * 16;
-    const bool act = !(d.nsrc > 1 && cn0 >= C0);    // src0 (activation) or src1 (stored: copied)
+    // src0 (activation) or, for SK_ACT_PLAIN, src1 (stored: copied)
+    const bool act = SK == SK_ACT || !(d.nsrc > 1 && cn0 >= C0);
+    const bool rag = cn0 + 16 > C0;
     const unsigned char* rb = raw_buf(q.s2);
     unsigned char* cb = comp_buf(q.s2);
     const float* tab = reinterpret_cast<const float*>(lds + Lay::OFF_TAB);
 #pragma unroll
     for (int k = 0; k < DPW; ++k) {
       const int i = wave + k * C5_NW;
-      if (i < NI) {
-        const int s = i * 64 + lane;
-        uint4 q4 = *reinterpret_cast<const uint4*>(rb + s * 16);
-        if (act) {
-          const int y = q.h0 + soy[k], x = q.w0 + sox[k], ch = cn0 + 8 * hbit[k];
-          const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W) & (ch < C0);
-          const int cc = ok ? ch : 0;
-          const float4 a0 = *reinterpret_cast<const float4*>(tab + cc);
-          const float4 a1 = *reinterpret_cast<const float4*>(tab + cc + 4);
-          const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_CMAX + cc);
-          const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_CMAX + cc + 4);
-          const float sc[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-          const float sf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-          float gm = ok ? 1.f : 0.f;
-          if (gated) {
-            const float pv = *reinterpret_cast<const float*>(gate_buf(q.ti) + i * 256 + lane * 4);
-            gm = ok ? sigmoidf_(pv * ga + gb) : 0.f;
-          }
-          float v[8];
-          unpack8_16<T>(q4, v);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo) * gm;
-          q4 = pack8_16<T>(v);
-          // act_out: the first output-channel block writes the transformed interior once (the weight
-          // gradient then reads it as a stored map) — a buffer store per slot, out-of-range for halo and
-          // padding slots, so every transform of an activation chunk issues exactly DPW (ns_prev: the next
-          // chunk's wait leaves them in flight)
-          if constexpr (OM == OM5_Y) {
-            if (aout) {
-              const bool in = ok && (unsigned)soy[k] < (unsigned)TH && (unsigned)sox[k] < (unsigned)C5_W;
-              const unsigned vo = in ? ((((unsigned)q.n * d.H + y) * (unsigned)d.W + x) * (unsigned)C0 + ch) * 2u : OOB;
-              typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q4), rao, (int)vo, 0, 0);
-            }
-          }
+      const bool live = i < NI;                      // slots past the image: the junk region (no branch)
+      const int s = i * 64 + lane;
+      const unsigned so = live ? (unsigned)s * 16u : (unsigned)(Lay::OFF_JUNK + lane * 16);
+      uint4 q4 = *reinterpret_cast<const uint4*>((live ? rb : lds) + so);
+      if (act) {
+        const int ch = cn0 + 8 * hbit[k];           // < C0 + 8: the table is zero-padded there
+        const bool ok = xok[k] && !(rag && hbit[k]);
+        const float4 a0 = *reinterpret_cast<const float4*>(tab + ch);
+        const float4 a1 = *reinterpret_cast<const float4*>(tab + ch + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_CMAX + ch);
+        const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_CMAX + ch + 4);
+        const f2_t sc[4] = {{a0.x, a0.y}, {a0.z, a0.w}, {a1.x, a1.y}, {a1.z, a1.w}};
+        const f2_t sf[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
+        float gm = ok ? 1.f : 0.f;
+        if constexpr (gated) {
+          const float pv = *reinterpret_cast<const float*>(gate_buf(q.ti) + (live ? i : 0) * 256 + lane * 4);
+          gm = ok ? sigmoidf_(pv * ga + gb) : 0.f;
         }
-        *reinterpret_cast<uint4*>(cb + s * 16) = q4;
-      } else if constexpr (OM == OM5_Y) {
-        if (aout && act) {
+        const f2_t g2 = {gm, gm};
+        float v[8];
+        unpack8_16<T>(q4, v);
+        unsigned u[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f2_t x2 = {v[2 * j], v[2 * j + 1]};
+          const f2_t t2 = __builtin_elementwise_fma(x2, sc[j], sf[j]) * g2;
+          u[j] = __builtin_bit_cast(unsigned, __builtin_elementwise_max(
+                                                  __builtin_bit_cast(s2_t, pack2_16<T>(t2.x, t2.y)), lo2));
+        }
+        q4 = make_uint4(u[0], u[1], u[2], u[3]);
+        // act_out: the first output-channel block writes the transformed interior once (the weight
+        // gradient then reads it as a stored map) — a buffer store per slot, out-of-range for halo, padding
+        // and dead slots and in the other blocks (zero-size resource), so every transform of an activation
+        // chunk issues exactly DPW (ns_prev: the next chunk's wait leaves them in flight)
+        if constexpr (OM == OM5_Y) {
+          const unsigned vo = (!live || (rag && hbit[k])) ? OOB : xao[k] + (unsigned)cn0 * 2u;
           typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, rao, (int)OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q4), rao, (int)vo, 0, 0);
         }
       }
+      *reinterpret_cast<uint4*>((live ? cb : lds) + so) = q4;
     }
-    if constexpr (OM == OM5_Y) ns_prev = aout && act;
+    if constexpr (OM == OM5_Y) ns_prev = act;
   };
 
   // ---- prologue: scale/shift table, chunks 0-2 in flight, chunk 0 ready ----
@@ -385,6 +421,22 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   };
 
   F xA[MI + 2], wA[3], xB[MI + 2], wB[3];
+  // PIPE 1: the operands of tap column dx+1 are read from LDS while the MFMAs of column dx run (pinned
+  // one ds_read per MFMA by sched_group_barrier), and column 0 of the next chunk right after the barrier.
+  // hipcc's own schedule (PIPE 0) read every fragment just before its MFMA with an lgkmcnt(0) in between,
+  // which exposed the LDS latency ~12 times per chunk: the bare MFMA + LDS loop (every ABL bit) ran at 50 %
+  // of the bf16 peak (profiles/r03_conv5_ablate.txt)
+  auto pin_col = [&]() {
+    if constexpr (PIPE) {
+#pragma unroll
+      for (int i = 0; i < MI + 5; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 3 * MI - (MI + 5), 0);
+    }
+  };
+  if constexpr (PIPE) load_col(K, 0, xA, wA);
   // BNB: the activation y1 of this wave's tile pixels (buffer loads, out-of-range offsets for masked lanes:
   // a fixed count), loaded during the tile's last chunk so that the epilogue's wait for them does not drain
   // the next chunks' DMAs (their issue follows the epilogue)
@@ -418,10 +470,19 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       if constexpr (OM == OM5_BNB) {
         if (last) load_y1(ti);
       }
-      load_col(K, 0, xA, wA);
-      mma_col(xA, wA);
-      load_col(K, 1, xB, wB);
-      mma_col(xB, wB);
+      if constexpr (PIPE) {
+        load_col(K, 1, xB, wB);
+        mma_col(xA, wA);
+        pin_col();
+        load_col(K, 2, xA, wA);
+        mma_col(xB, wB);
+        pin_col();
+      } else {
+        load_col(K, 0, xA, wA);
+        mma_col(xA, wA);
+        load_col(K, 1, xB, wB);
+        mma_col(xB, wB);
+      }
       wait_next(last);
       if constexpr (ACT && !(ABL & 16)) {
         if (X.ti < ntl) {
@@ -429,11 +490,13 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
           cur_next(X);
         }
       }
-      load_col(K, 2, xA, wA);
+      if constexpr (!PIPE) load_col(K, 2, xA, wA);
       mma_col(xA, wA);
       if constexpr (!(ABL & 8)) lds_barrier();
       if (OM != OM5_BNB || !last) issue_next();
       cur_next(K);
+      // the next chunk's column 0 (past the block's last chunk: harmless reads of stale LDS)
+      if constexpr (PIPE) load_col(K, 0, xA, wA);
     }
 
     // ---------------- epilogue of tile ti ----------------
@@ -694,45 +757,63 @@ int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
   return 0;
 }
 
-template <typename T, int OM, int SK, int ABL = 0>
+// UNET_CONV5_PIPE=0: the round-3 chunk loop (hipcc's operand schedule), for A/B runs
+static bool conv5_pipe() {
+  const char* e = getenv("UNET_CONV5_PIPE");
+  return !e || atoi(e) != 0;
+}
+
+template <typename T, int OM, int SK, int GATE, int ABL = 0>
 static int launch5(const unet_conv_desc* d, hipStream_t st) {
   constexpr int TH = C5_WM * C5_MI;
   const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH);
   const int mt = d->N * tw * th;
   const int gy = cdiv(d->Cout, C5_BN);
   const int gx = conv5_gx(d);
-  hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, ABL>), dim3(gx, gy), dim3(C5_NT), 0, st, *d, tw, th, mt,
-                     cdiv(d->Cin, 16));
+  if (conv5_pipe())
+    hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, 1>), dim3(gx, gy), dim3(C5_NT), 0, st, *d, tw, th,
+                       mt, cdiv(d->Cin, 16));
+  else
+    hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, 0>), dim3(gx, gy), dim3(C5_NT), 0, st, *d, tw, th,
+                       mt, cdiv(d->Cin, 16));
   return check_launch("conv5");
+}
+
+// source kind of a descriptor: plain, one BN activation (gated or not), or a BN activation + a stored map.
+// The gradient epilogues (whose network sources are the stored dy) get the generic activation form only.
+template <typename T, int OM>
+static int dispatch5_om(const unet_conv_desc* d, hipStream_t st) {
+  const unet_src& s0 = d->src[0];
+  if (s0.kind != UNET_SRC_ACT) return launch5<T, OM, SK_PLAIN, 0>(d, st);
+  const bool g = s0.gate_p != nullptr;
+  if (OM == OM5_Y && d->nsrc == 1) return g ? launch5<T, OM, SK_ACT, 1>(d, st) : launch5<T, OM, SK_ACT, 0>(d, st);
+  return g ? launch5<T, OM, SK_ACT_PLAIN, 1>(d, st) : launch5<T, OM, SK_ACT_PLAIN, 0>(d, st);
 }
 
 template <typename T>
 static int dispatch5(const unet_conv_desc* d, hipStream_t st) {
-  const bool act = d->src[0].kind == UNET_SRC_ACT;
-  if (d->out_mode == UNET_OUT_F32)
-    return act ? launch5<T, OM5_F32, SK_ACT>(d, st) : launch5<T, OM5_F32, SK_PLAIN>(d, st);
-  if (d->bnb_stats)
-    return act ? launch5<T, OM5_BNB, SK_ACT>(d, st) : launch5<T, OM5_BNB, SK_PLAIN>(d, st);
-  return act ? launch5<T, OM5_Y, SK_ACT>(d, st) : launch5<T, OM5_Y, SK_PLAIN>(d, st);
+  if (d->out_mode == UNET_OUT_F32) return dispatch5_om<T, OM5_F32>(d, st);
+  if (d->bnb_stats) return dispatch5_om<T, OM5_BNB>(d, st);
+  return dispatch5_om<T, OM5_Y>(d, st);
 }
 
 int conv5_run(const unet_conv_desc* d, hipStream_t st) {
   return d->dtype == UNET_F16 ? dispatch5<f16>(d, st) : dispatch5<bf16>(d, st);
 }
 
-template <int SK>
+template <int SK, int GATE>
 static int abl5(const unet_conv_desc* d, int abl, hipStream_t st) {
   switch (abl) {
-    case 0: return launch5<bf16, OM5_Y, SK, 0>(d, st);
-    case 1: return launch5<bf16, OM5_Y, SK, 1>(d, st);
-    case 2: return launch5<bf16, OM5_Y, SK, 2>(d, st);
-    case 3: return launch5<bf16, OM5_Y, SK, 3>(d, st);
-    case 4: return launch5<bf16, OM5_Y, SK, 4>(d, st);
-    case 8: return launch5<bf16, OM5_Y, SK, 8>(d, st);
-    case 7: return launch5<bf16, OM5_Y, SK, 7>(d, st);
-    case 15: return launch5<bf16, OM5_Y, SK, 15>(d, st);
-    case 16: return launch5<bf16, OM5_Y, SK, 16>(d, st);
-    case 31: return launch5<bf16, OM5_Y, SK, 31>(d, st);
+    case 0: return launch5<bf16, OM5_Y, SK, GATE, 0>(d, st);
+    case 1: return launch5<bf16, OM5_Y, SK, GATE, 1>(d, st);
+    case 2: return launch5<bf16, OM5_Y, SK, GATE, 2>(d, st);
+    case 3: return launch5<bf16, OM5_Y, SK, GATE, 3>(d, st);
+    case 4: return launch5<bf16, OM5_Y, SK, GATE, 4>(d, st);
+    case 8: return launch5<bf16, OM5_Y, SK, GATE, 8>(d, st);
+    case 7: return launch5<bf16, OM5_Y, SK, GATE, 7>(d, st);
+    case 15: return launch5<bf16, OM5_Y, SK, GATE, 15>(d, st);
+    case 16: return launch5<bf16, OM5_Y, SK, GATE, 16>(d, st);
+    case 31: return launch5<bf16, OM5_Y, SK, GATE, 31>(d, st);
   }
   return UNET_ERR_ARG;
 }
@@ -745,5 +826,5 @@ extern "C" int unet_diag_conv5_ablate(const unet_conv_desc* d, int abl, void* st
   using namespace unet;
   if (!conv5_eligible(d) || d->nsrc != 1 || d->out_mode != UNET_OUT_Y || d->dtype != UNET_BF16) return UNET_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  return d->src[0].kind == UNET_SRC_PLAIN ? abl5<SK_PLAIN>(d, abl, st) : abl5<SK_ACT>(d, abl, st);
+  return d->src[0].kind == UNET_SRC_PLAIN ? abl5<SK_PLAIN, 0>(d, abl, st) : abl5<SK_ACT, 0>(d, abl, st);
 }

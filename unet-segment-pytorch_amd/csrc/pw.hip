@@ -48,10 +48,13 @@ __device__ __forceinline__ typename Mma<T>::frag pw_act(uint4 q, bool act, const
 // ------------------------------------------------------------------------------------------------
 // fwd / dgrad.  Block = 4 waves; wave = 16*NB pixels x 16*NA output channels; grid (P / (64*NB), Cout / (16*NA))
 // ------------------------------------------------------------------------------------------------
-// GATED (UNET_OUT_F32_GATED): the attention gate's W_x input gradient, with the x*s term of the same
-// gradient added here instead of by gate_bwd1: d(x*s) and s = sigmoid(psi) are loaded ahead of the MFMAs
-template <typename T, int NA, int NB, bool GATED = false>
+// OMK: the output mode at compile time (0: y + BN partial sums, 1: fp32 gradient, 2: UNET_OUT_F32_GATED — the
+// attention gate's W_x input gradient, with the x*s term of the same gradient added here instead of by
+// gate_bwd1: d(x*s) and s = sigmoid(psi) are loaded ahead of the MFMAs).  Distinct instantiations also keep
+// the forward and the dgrads apart in kernel traces and PMC passes (tools/traffic.py)
+template <typename T, int NA, int NB, int OMK>
 __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, long long P, int nchunks) {
+  constexpr bool GATED = OMK == 2;
   typedef typename Mma<T>::frag F;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i16 = lane & 15, g = lane >> 4;
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
   // compiler cannot hoist them over the stores, which it must assume alias; loaded in the epilogue, each
   // read-modify-write was a full memory round trip per 16-byte column)
   float4 old[NB][NA];
-  const bool rmw = !GATED && d.out_mode == UNET_OUT_F32 && (d.accum || d.accum2);
+  const bool rmw = OMK == 1 && (d.accum || d.accum2);
   float4 gxs[GATED ? NB : 1][GATED ? NA : 1];
   float gsv[GATED ? NB : 1];
   if constexpr (GATED) {
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
   }
 
   // epilogue: acc[a][b][r] = out[px = pw0 + 16b + i16][co = co0 + 16a + 4g + r]
-  if (d.out_mode == UNET_OUT_Y) {
+  if constexpr (OMK == 0) {
     T* y = (T*)d.out;
     float sm[NA][4], sq[NA][4];
 #pragma unroll
@@ -516,9 +519,11 @@ static int launch_pw(const unet_conv_desc* d, hipStream_t st) {
   const long long P = (long long)d->N * d->H * d->W;
   dim3 grid(cdiv(P, 64 * NB), d->Cout / (16 * NA));
   if (d->out_mode == UNET_OUT_F32_GATED)
-    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, true>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 2>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+  else if (d->out_mode == UNET_OUT_F32)
+    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 1>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
   else
-    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 0>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
   return check_launch("pw_conv");
 }
 
