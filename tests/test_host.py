@@ -138,3 +138,22 @@ def test_graphed_train_step_rejects_other_optimizers():
         GraphedTrainStep(m, DiceBCELoss(), torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9), (1, 1, 8, 8), (1, 8, 8))
     with pytest.raises(RuntimeError, match="capturable"):
         GraphedTrainStep(m, DiceBCELoss(), torch.optim.AdamW(m.parameters(), lr=1e-3), (1, 1, 8, 8), (1, 8, 8))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_relu_after_16bit_rounding_identity(dt):
+    """conv5 / wgrad5 apply the BN-activation's ReLU after the 16-bit rounding, as a signed 16-bit integer max
+    against 0 on the packed result (v_pk_max_i16): for a multiplier g >= 0 (the attention gate's sigmoid, or the
+    0 / 1 zero-padding mask), max_i16(round16(t * g), 0) has the bits of round16(max(t, 0) * g), the round-3
+    order, except that a negative zero becomes +0 (which no sum can tell apart)."""
+    g = torch.Generator().manual_seed(5)
+    t = torch.randn(200000, generator=g) * torch.exp(torch.randn(200000, generator=g) * 4)
+    m = torch.rand(200000, generator=g)
+    m[::7] = 0.0
+    m[::11] = 1.0
+    ref = (torch.clamp(t, min=0.0) * m).to(dt)
+    new_bits = torch.clamp((t * m).to(dt).view(torch.int16), min=0)
+    ref_bits = ref.view(torch.int16)
+    # -0.0 (0x8000) in the reference is +0 in the new order
+    ref_bits = torch.where(ref_bits == -32768, torch.zeros_like(ref_bits), ref_bits)
+    assert torch.equal(new_bits, ref_bits)

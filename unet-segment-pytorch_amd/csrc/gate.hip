@@ -125,6 +125,8 @@ __device__ __forceinline__ void load8(const T* p, float* v) {
   }
 }
 
+constexpr int GV_U = 4;    // pixels per lane per trip of the vectorised gate passes (loads in flight)
+
 template <typename T>
 __global__ void psi_vec_kernel(long long P, int Ci, int G, const T* __restrict__ gw, const T* __restrict__ xw,
                                const float* gab, const float* xab, const float* wpsi, float* __restrict__ p, float* part,
@@ -141,18 +143,28 @@ __global__ void psi_vec_kernel(long long P, int Ci, int G, const T* __restrict__
   const long long per = (P + rows - 1) / rows;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
   float s = 0.f, ss = 0.f;
-  for (long long q = p0 + wave * ppw + lane / G; q < p1; q += (long long)nw * ppw) {
-    float g[8], x[8];
-    load8<T>(gw + q * Ci + c0, g);
-    load8<T>(xw + q * Ci + c0, x);
-    float acc = 0.f;
+  // GV_U pixels per lane per trip, every load issued first (one pixel per trip serialised a memory round
+  // trip per pixel); the pixels are then reduced in the one-pixel loop's order, so s / ss are unchanged
+  const long long S = (long long)nw * ppw;
+  for (long long q = p0 + wave * ppw + lane / G; q < p1; q += GV_U * S) {
+    float g[GV_U][8], x[GV_U][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += w[j] * fmaxf(g[j] * gs[j] + gb[j] + x[j] * xs[j] + xb[j], 0.f);
-    acc = group_sum(acc, G);
-    if (sub == 0) {
-      p[q] = acc;
-      s += acc;
-      ss += acc * acc;
+    for (int u = 0; u < GV_U; ++u) {
+      const long long qq = q + u * S < p1 ? q + u * S : q;
+      load8<T>(gw + qq * Ci + c0, g[u]);
+      load8<T>(xw + qq * Ci + c0, x[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < GV_U; ++u) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += w[j] * fmaxf(g[u][j] * gs[j] + gb[j] + x[u][j] * xs[j] + xb[j], 0.f);
+      acc = group_sum(acc, G);
+      if (sub == 0 && q + u * S < p1) {
+        p[q + u * S] = acc;
+        s += acc;
+        ss += acc * acc;
+      }
     }
   }
   s = block_sum_f(s, sh);
@@ -356,19 +368,30 @@ __global__ __launch_bounds__(256) void gate_bwd2_vec_kernel(long long P, int Ci,
   float a0[8], a1[8], a2[8], a3[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { a0[j] = 0.f; a1[j] = 0.f; a2[j] = 0.f; a3[j] = 0.f; }
-  for (long long q = p0 + tid / G; q < p1; q += slots) {
-    float g[8], x[8];
-    load8<T>(gw + q * Ci + c0, g);
-    load8<T>(xw + q * Ci + c0, x);
-    const float dp = A * dq[q] + B * pp[q] + Cc;
+  // GV_U pixels per trip, loads first, summed in the one-pixel loop's order (bit-identical sums)
+  for (long long q = p0 + tid / G; q < p1; q += GV_U * slots) {
+    float g[GV_U][8], x[GV_U][8], dqv[GV_U], ppv[GV_U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float a = fmaxf(g[j] * gs[j] + gb[j] + x[j] * xs[j] + xb[j], 0.f);
-      const float dz = a > 0.f ? dp * w[j] : 0.f;
-      a0[j] += dz;
-      a1[j] += dz * (g[j] - gmu[j]) * giv[j];
-      a2[j] += dz * (x[j] - xmu[j]) * xiv[j];
-      a3[j] += dp * a;
+    for (int u = 0; u < GV_U; ++u) {
+      const long long qq = q + u * slots < p1 ? q + u * slots : q;
+      load8<T>(gw + qq * Ci + c0, g[u]);
+      load8<T>(xw + qq * Ci + c0, x[u]);
+      dqv[u] = dq[qq];
+      ppv[u] = pp[qq];
+    }
+#pragma unroll
+    for (int u = 0; u < GV_U; ++u) {
+      if (q + u * slots >= p1) break;
+      const float dp = A * dqv[u] + B * ppv[u] + Cc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = fmaxf(g[u][j] * gs[j] + gb[j] + x[u][j] * xs[j] + xb[j], 0.f);
+        const float dz = a > 0.f ? dp * w[j] : 0.f;
+        a0[j] += dz;
+        a1[j] += dz * (g[u][j] - gmu[j]) * giv[j];
+        a2[j] += dz * (x[u][j] - xmu[j]) * xiv[j];
+        a3[j] += dp * a;
+      }
     }
   }
 #pragma unroll
@@ -413,20 +436,32 @@ __global__ __launch_bounds__(256) void gate_bwd3_vec_kernel(long long P, int Ci,
   const float A = pc[0], B = pc[1], Cc = pc[2];
   const long long per = (P + rows - 1) / rows;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  for (long long q = p0 + tid / G; q < p1; q += slots) {
-    float g[8], x[8], og[8], ox[8];
-    load8<T>(gw + q * Ci + c0, g);
-    load8<T>(xw + q * Ci + c0, x);
-    const float dp = A * dq[q] + B * pp[q] + Cc;
+  for (long long q = p0 + tid / G; q < p1; q += GV_U * slots) {
+    float g[GV_U][8], x[GV_U][8], dqv[GV_U], ppv[GV_U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float a = fmaxf(g[j] * gs[j] + gb[j] + x[j] * xs[j] + xb[j], 0.f);
-      const float dz = a > 0.f ? dp * w[j] : 0.f;
-      og[j] = gA[j] * dz + gB[j] * g[j] + gC[j];
-      ox[j] = xA[j] * dz + xB[j] * x[j] + xC[j];
+    for (int u = 0; u < GV_U; ++u) {
+      const long long qq = q + u * slots < p1 ? q + u * slots : q;
+      load8<T>(gw + qq * Ci + c0, g[u]);
+      load8<T>(xw + qq * Ci + c0, x[u]);
+      dqv[u] = dq[qq];
+      ppv[u] = pp[qq];
     }
-    store8<T>(dgw + q * Ci + c0, og);
-    store8<T>(dxw + q * Ci + c0, ox);
+#pragma unroll
+    for (int u = 0; u < GV_U; ++u) {
+      const long long qq = q + u * slots;
+      if (qq >= p1) break;
+      float og[8], ox[8];
+      const float dp = A * dqv[u] + B * ppv[u] + Cc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = fmaxf(g[u][j] * gs[j] + gb[j] + x[u][j] * xs[j] + xb[j], 0.f);
+        const float dz = a > 0.f ? dp * w[j] : 0.f;
+        og[j] = gA[j] * dz + gB[j] * g[u][j] + gC[j];
+        ox[j] = xA[j] * dz + xB[j] * x[u][j] + xC[j];
+      }
+      store8<T>(dgw + qq * Ci + c0, og);
+      store8<T>(dxw + qq * Ci + c0, ox);
+    }
   }
 }
 

@@ -112,7 +112,6 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
   const rsrc4_t rsg = mk_rsrc4(gated ? (const void*)s0.gate_p : d.dy, (unsigned)(npix * 4));
   float ga = 0.f, gb = 0.f;
   if (gated) { ga = s0.gate_ab[0]; gb = s0.gate_ab[1]; }
-  const float lo = s0.relu ? 0.f : -INFINITY;
   if constexpr (ACT) {
     // scale / shift of the block's BCI channels (ordinary loads, before any DMA is in flight)
     float* tab = reinterpret_cast<float*>(lds + Lay::OFF_TAB);
@@ -236,7 +235,12 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
   };
 
   // BN-activation (+gate) transform of the halo at cursor c, raw -> compute image, this lane's own slots
-  // (zero padding and the image's tail come out 0; a block on the stored concat source copies)
+  // (zero padding and the image's tail come out 0; a block on the stored concat source copies).  Packed as in
+  // conv5.hip: v_pk_fma_f32 / v_pk_mul_f32 on channel pairs, ReLU as v_pk_max_i16 against 0 after the 16-bit
+  // rounding (the same bits up to the sign of zero); slots past the image use the junk region (no branch)
+  typedef __attribute__((ext_vector_type(2))) float f2_t;
+  typedef __attribute__((ext_vector_type(2))) short s2_t;
+  const s2_t lo2 = s0.relu ? s2_t{0, 0} : s2_t{-32768, -32768};
   auto transform = [&](const Cur& c) {
     const unsigned char* rb = lds + Lay::OFF_RAW + c.s2 * Lay::XIMG;
     unsigned char* cb = lds + Lay::OFF_X + c.s2 * Lay::XIMG;
@@ -244,33 +248,40 @@ __global__ __launch_bounds__(W5_NT, 1) void wgrad5_kernel(const unet_wgrad_desc 
 #pragma unroll
     for (int k = 0; k < DPWX; ++k) {
       const int i = wave + k * W5_NW;
-      if (i < NIX) {
-        const int s = i * 64 + lane;
-        uint4 q4 = *reinterpret_cast<const uint4*>(rb + s * 16);
-        if (xact) {
-          const int y = c.h0 + xrow[k], x = c.w0 + xcol[k];
-          const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
-          const int cc = xch[k];
-          const float4 a0 = *reinterpret_cast<const float4*>(tab + cc);
-          const float4 a1 = *reinterpret_cast<const float4*>(tab + cc + 4);
-          const float4 b0 = *reinterpret_cast<const float4*>(tab + BCI + cc);
-          const float4 b1 = *reinterpret_cast<const float4*>(tab + BCI + cc + 4);
-          const float sc[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-          const float sf[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-          float gm = ok ? 1.f : 0.f;
-          if (gated) {
-            const float pv = *reinterpret_cast<const float*>(lds + Lay::OFF_GATE + c.s2 * Lay::GATE + wave * 256 +
-                                                             (k * 8 + (lane >> 3)) * 4);
-            gm = ok ? sigmoidf_(pv * ga + gb) : 0.f;
-          }
-          float v[8];
-          unpack8_16<T>(q4, v);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo) * gm;
-          q4 = pack8_16<T>(v);
+      const bool live = i < NIX;
+      const int s = i * 64 + lane;
+      const unsigned so = live ? (unsigned)s * 16u : (unsigned)(Lay::OFF_JUNK + lane * 16);
+      uint4 q4 = *reinterpret_cast<const uint4*>((live ? rb : lds) + so);
+      if (xact) {
+        const int y = c.h0 + xrow[k], x = c.w0 + xcol[k];
+        const bool ok = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
+        const int cc = xch[k];
+        const float4 a0 = *reinterpret_cast<const float4*>(tab + cc);
+        const float4 a1 = *reinterpret_cast<const float4*>(tab + cc + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(tab + BCI + cc);
+        const float4 b1 = *reinterpret_cast<const float4*>(tab + BCI + cc + 4);
+        const f2_t sc[4] = {{a0.x, a0.y}, {a0.z, a0.w}, {a1.x, a1.y}, {a1.z, a1.w}};
+        const f2_t sf[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
+        float gm = ok ? 1.f : 0.f;
+        if (gated) {
+          const float pv = *reinterpret_cast<const float*>(lds + Lay::OFF_GATE + c.s2 * Lay::GATE + wave * 256 +
+                                                           (k * 8 + (lane >> 3)) * 4);
+          gm = ok ? sigmoidf_(pv * ga + gb) : 0.f;
         }
-        *reinterpret_cast<uint4*>(cb + s * 16) = q4;
+        const f2_t g2 = {gm, gm};
+        float v[8];
+        unpack8_16<T>(q4, v);
+        unsigned u[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f2_t x2 = {v[2 * j], v[2 * j + 1]};
+          const f2_t t2 = __builtin_elementwise_fma(x2, sc[j], sf[j]) * g2;
+          u[j] = __builtin_bit_cast(unsigned, __builtin_elementwise_max(
+                                                  __builtin_bit_cast(s2_t, pack2_16<T>(t2.x, t2.y)), lo2));
+        }
+        q4 = make_uint4(u[0], u[1], u[2], u[3]);
       }
+      *reinterpret_cast<uint4*>((live ? cb : lds) + so) = q4;
     }
   };
 
