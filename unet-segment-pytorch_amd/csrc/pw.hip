@@ -173,19 +173,38 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const long long p = pw0 + 16 * b + i16;
+      if constexpr (NA % 2 == 0) {
+        // lane (i16, g) holds channels 16 a + 4 g .. + 3 of pixel p: v_permlane16_swap of the packed (a, a + 1)
+        // pairs leaves row g with the 8 contiguous channels 16 (a + (g & 1)) + 8 (g >> 1) .. + 7, stored as one
+        // 16-byte vector (smallcin.hip's epilogue); every lane takes part in the swaps, the stores are masked
 #pragma unroll
-      for (int a = 0; a < NA; ++a) {
-        const int co = co0 + 16 * a + 4 * g;
-        if (p < P) {
-          const f32x4 v = acc[a][b];
-          *reinterpret_cast<uint2*>(y + p * d.Cout + co) = make_uint2(pack2_16<T>(v[0], v[1]), pack2_16<T>(v[2], v[3]));
+        for (int a = 0; a < NA; a += 2) {
+          const f32x4 v0 = acc[a][b], v1 = acc[a + 1][b];
+          const auto sx = __builtin_amdgcn_permlane16_swap(pack2_16<T>(v0[0], v0[1]), pack2_16<T>(v1[0], v1[1]),
+                                                           false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(pack2_16<T>(v0[2], v0[3]), pack2_16<T>(v1[2], v1[3]),
+                                                           false, false);
+          if (p < P)
+            *reinterpret_cast<uint4*>(y + p * d.Cout + co0 + 16 * (a + (g & 1)) + 8 * (g >> 1)) =
+                make_uint4(sx[0], sy[0], sx[1], sy[1]);
         }
+      } else {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          const int co = co0 + 16 * a + 4 * g;
+          if (p < P) {
+            const f32x4 v = acc[a][b];
+            *reinterpret_cast<uint2*>(y + p * d.Cout + co) = make_uint2(pack2_16<T>(v[0], v[1]), pack2_16<T>(v[2], v[3]));
+          }
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {  // pixels past P accumulated exact zeros
           sm[a][r] += acc[a][b][r];
           sq[a][r] += acc[a][b][r] * acc[a][b][r];
         }
-      }
     }
     if (d.stats) {
       __shared__ float red[4][NA * 16][2];

@@ -378,20 +378,33 @@ __global__ __launch_bounds__(256) void smallcin_fwd_mfma_kernel(const unet_conv_
           for (int f = 0; f < 4; ++f) acc[f] = Mma<T>::mma(a[ks][f], b, acc[f]);
         }
       }
-      if (ow < d.W) {
-        const size_t pix = ((size_t)n * d.H + h0 + r) * d.W + ow;
+      // lane (c16, g) holds channels 16 f + 4 g .. + 3 of pixel ow for f = 0..3.  v_permlane16_swap of the
+      // packed (f, f + 1) pairs (odd rows of the first with even rows of the second) leaves row g with the
+      // 8 contiguous channels 16 (f + (g & 1)) + 8 (g >> 1) .. + 7: two 16-byte stores per lane and row
+      // instead of four 8-byte ones (all lanes take part in the swaps; the stores are masked)
+      unsigned px_[4], py_[4];
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          uint2 pk;
-          pk.x = pack2_16<T>(acc[f][0], acc[f][1]);
-          pk.y = pack2_16<T>(acc[f][2], acc[f][3]);
-          *reinterpret_cast<uint2*>(y + pix * 64 + 16 * f + 4 * g) = pk;
+      for (int f = 0; f < 4; ++f) {
+        px_[f] = pack2_16<T>(acc[f][0], acc[f][1]);
+        py_[f] = pack2_16<T>(acc[f][2], acc[f][3]);
+      }
+      const size_t pix = ((size_t)n * d.H + h0 + r) * d.W + ow;
+#pragma unroll
+      for (int f = 0; f < 4; f += 2) {
+        const auto sx = __builtin_amdgcn_permlane16_swap(px_[f], px_[f + 1], false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(py_[f], py_[f + 1], false, false);
+        if (ow < d.W)
+          *reinterpret_cast<uint4*>(y + pix * 64 + 16 * (f + (g & 1)) + 8 * (g >> 1)) =
+              make_uint4(sx[0], sy[0], sx[1], sy[1]);
+      }
+      if (ow < d.W) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             s1[f][q] += acc[f][q];
             s2[f][q] = __builtin_fmaf(acc[f][q], acc[f][q], s2[f][q]);
           }
-        }
       }
     }
   }
