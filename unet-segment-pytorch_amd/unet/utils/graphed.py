@@ -18,13 +18,16 @@ with a scheduler (scripts/train.py:353-370), give the optimizer a device tensor 
 (`AdamW(..., lr=torch.tensor(1e-3, device="cuda"), capturable=True)`): the fused step reads it from device
 memory on every replay, and torch's LR schedulers update a tensor lr in place.
 
-Gradients: the backward is taken with torch.autograd.grad over the parameters (no AccumulateGrad nodes
-run), and the results are assigned to `p.grad`.  That matters when the caller still holds an eager step's
-autograd graph (e.g. its `loss`): its AccumulateGrad nodes were created on the default stream, stay
-attached to the parameters while that graph lives, and a `.backward()` inside the capture would route the
-gradient of every parameter through them — a cross-stream wait on the default stream in the middle of a
-stream capture ("GraphedTrainStep and a live eager graph").  Values are identical: every
-parameter gets exactly one gradient per step, which AccumulateGrad would only have stored.
+Gradients: the captured forward runs on leaf aliases of the parameters (`p.detach().requires_grad_()`: the
+same storage, so the optimizer's in-place updates are what the next replay reads) through
+torch.func.functional_call, and the backward is torch.autograd.grad over those aliases; the results are
+assigned to `p.grad`.  That matters when the caller still holds an eager step's autograd graph (e.g. its
+`loss`): a parameter's AccumulateGrad node lives as long as that graph and is bound to the stream it was
+created on (the default stream); a capture whose graph reaches it makes the engine sync the capture stream
+with the default stream, and torch.cuda.graph's capture_end then crashed the process (segfault, round 3 and
+tests/test_gpu_graphed.py on the round-3 code; DESIGN.md §7, "GraphedTrainStep and a live eager graph").  The
+aliases' own AccumulateGrad nodes are created inside the capture.  Values are identical: every parameter
+gets exactly one gradient per step, which AccumulateGrad would only have stored.
 
 Weights, BN running statistics and optimizer state live in their own tensors and are updated in place by
 every replay; `loss` is a device tensor that every replay overwrites; `p.grad` are the step's gradients
@@ -36,6 +39,7 @@ from __future__ import annotations
 from typing import Callable, Optional, Sequence
 
 import torch
+from torch.func import functional_call
 
 
 def _frozen_hyperparameters(optimizer: torch.optim.Optimizer):
@@ -53,7 +57,11 @@ class GraphedTrainStep:
         if not all(g.get("capturable", False) for g in optimizer.param_groups):
             raise RuntimeError("GraphedTrainStep: the optimizer must be built with capturable=True")
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
-        self.params = [p for p in model.parameters() if p.requires_grad]
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        self.params = [p for _, p in named]
+        # leaf aliases (shared storage) the captured forward runs on: their AccumulateGrad nodes are the
+        # capture's own, whatever eager graph of the model the caller keeps alive
+        self.leaves = {n: p.detach().requires_grad_(True) for n, p in named}
         self.clip_norm = clip_norm
         self.x = torch.zeros(*input_shape, dtype=torch.float32, device=device)
         self.t = torch.zeros(*target_shape, dtype=target_dtype, device=device)
@@ -95,9 +103,9 @@ class GraphedTrainStep:
                 t.zero_()
 
     def _body(self) -> torch.Tensor:
-        loss = self.criterion(self.model(self.x), self.t)
-        # autograd.grad, not backward(): no AccumulateGrad node runs (see the module docstring)
-        grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        loss = self.criterion(functional_call(self.model, self.leaves, (self.x,)), self.t)
+        # autograd.grad over the aliases, not backward(): see the module docstring
+        grads = torch.autograd.grad(loss, list(self.leaves.values()), allow_unused=True)
         for p, g in zip(self.params, grads):
             p.grad = g
         if self.clip_norm is not None:
