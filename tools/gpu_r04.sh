@@ -52,14 +52,17 @@ for step in ${STEPS:-tests smoke bench}; do
   ablate)
     timeout -k 10 300 python -u tools/conv5_ablate.py ${ABL:-0,4,16,31} > $O/conv5_ablate.txt 2>&1 || fail ablate $O/conv5_ablate.txt
     cat $O/conv5_ablate.txt ;;
-  ab)      # A/B of an environment switch on one box: layer timing + the quick bench line, A then B then A
-    for v in "${ABA:-}" "${ABB:-}"; do
+  ab)      # A/B(/C) of environment switches on one box: layer timing + the quick bench line, A B (C) A
+    for v in "${ABA:-}" "${ABB:-}" ${ABC:+"$ABC"}; do
       env $v timeout -k 10 300 python -u tools/layerprof.py > "$O/layerprof_${v//[^A-Za-z0-9]/_}.txt" 2>&1 || fail "ab layerprof $v" "$O/layerprof_${v//[^A-Za-z0-9]/_}.txt"
     done
-    for v in "${ABA:-}" "${ABB:-}" "${ABA:-}"; do
+    for v in "${ABA:-}" "${ABB:-}" ${ABC:+"$ABC"} "${ABA:-}"; do
       env $v timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-fp32-line --no-graph-line > $O/ab.json 2> $O/ab.err || fail "ab bench $v" $O/ab.err
       echo "[$v] $(python -c "import json;d=json.load(open('$O/ab.json'));print(d['value'],d['ms_per_step'],d['roofline']['avg_us'])")"
     done ;;
+  gdiag)
+    timeout -k 10 180 python -u tools/graphed_diag.py > $O/graphed_diag.log 2>&1 || fail gdiag $O/graphed_diag.log 40
+    cat $O/graphed_diag.log | grep -v amdgpu.ids ;;
   repro)   # round 3's GraphedTrainStep crash (old capture path); last in a call: it may end in a segfault
     PYTHONFAULTHANDLER=1 timeout -k 10 180 python -u tools/repro_graphed_live_graph.py ${REPRO:-backward} > $O/repro.log 2>&1; echo "repro rc $?" >> $O/repro.log
     tail -40 $O/repro.log ;;

@@ -423,9 +423,8 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   F xA[MI + 2], wA[3], xB[MI + 2], wB[3];
   // PIPE 1: the operands of tap column dx+1 are read from LDS while the MFMAs of column dx run (pinned
   // one ds_read per MFMA by sched_group_barrier), and column 0 of the next chunk right after the barrier.
-  // hipcc's own schedule (PIPE 0) read every fragment just before its MFMA with an lgkmcnt(0) in between,
-  // which exposed the LDS latency ~12 times per chunk: the bare MFMA + LDS loop (every ABL bit) ran at 50 %
-  // of the bf16 peak (profiles/r03_conv5_ablate.txt)
+  // hipcc's own schedule (PIPE 0) reads every fragment just before its MFMA with an lgkmcnt(0) in between;
+  // PIPE 1 measured 5-9 % faster per layer for the y / fp32 epilogues (launch5)
   auto pin_col = [&]() {
     if constexpr (PIPE) {
 #pragma unroll
@@ -757,25 +756,20 @@ int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
   return 0;
 }
 
-// UNET_CONV5_PIPE=0: the round-3 chunk loop (hipcc's operand schedule), for A/B runs
-static bool conv5_pipe() {
-  const char* e = getenv("UNET_CONV5_PIPE");
-  return !e || atoi(e) != 0;
-}
-
+// PIPE: the column-ahead operand reads for the y and fp32 epilogues (per layer 5-9 % faster: 117 -> 108 us on
+// the 512^2 64->64 forward, profiles/r04_layerprof_conv5_pipe{0,1}.txt); the BN-backward-sums epilogue keeps
+// the compiler's schedule: with both operand columns and its 16 y1 registers live it ran out of VGPRs
+// (256 + 108 bytes of scratch) and went 14-30 % slower
 template <typename T, int OM, int SK, int GATE, int ABL = 0>
 static int launch5(const unet_conv_desc* d, hipStream_t st) {
   constexpr int TH = C5_WM * C5_MI;
+  constexpr int PIPE = OM == OM5_BNB ? 0 : 1;
   const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH);
   const int mt = d->N * tw * th;
   const int gy = cdiv(d->Cout, C5_BN);
   const int gx = conv5_gx(d);
-  if (conv5_pipe())
-    hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, 1>), dim3(gx, gy), dim3(C5_NT), 0, st, *d, tw, th,
-                       mt, cdiv(d->Cin, 16));
-  else
-    hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, 0>), dim3(gx, gy), dim3(C5_NT), 0, st, *d, tw, th,
-                       mt, cdiv(d->Cin, 16));
+  hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, PIPE>), dim3(gx, gy), dim3(C5_NT), 0, st, *d, tw, th,
+                     mt, cdiv(d->Cin, 16));
   return check_launch("conv5");
 }
 

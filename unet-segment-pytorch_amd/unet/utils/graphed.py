@@ -18,10 +18,11 @@ with a scheduler (scripts/train.py:353-370), give the optimizer a device tensor 
 (`AdamW(..., lr=torch.tensor(1e-3, device="cuda"), capturable=True)`): the fused step reads it from device
 memory on every replay, and torch's LR schedulers update a tensor lr in place.
 
-Gradients: the captured forward runs on leaf aliases of the parameters (`p.detach().requires_grad_()`: the
-same storage, so the optimizer's in-place updates are what the next replay reads) through
-torch.func.functional_call, and the backward is torch.autograd.grad over those aliases; the results are
-assigned to `p.grad`.  That matters when the caller still holds an eager step's autograd graph (e.g. its
+Gradients: the captured forward AND backward run with the model's parameters swapped for leaf aliases
+(`p.detach().requires_grad_()`: the same storage, so the optimizer's in-place updates are what the next replay
+reads; swapped in `module._parameters` for the duration of the step, as torch.func.functional_call does, but
+around the backward too: the HIP stages look their parameters up again when their backward runs), and the
+backward is torch.autograd.grad over those aliases; the results are assigned to `p.grad`.  That matters when the caller still holds an eager step's autograd graph (e.g. its
 `loss`): a parameter's AccumulateGrad node lives as long as that graph and is bound to the stream it was
 created on (the default stream); a capture whose graph reaches it makes the engine sync the capture stream
 with the default stream, and torch.cuda.graph's capture_end then crashed the process (segfault, round 3 and
@@ -36,15 +37,33 @@ every replay; `loss` is a device tensor that every replay overwrites; `p.grad` a
 
 from __future__ import annotations
 
+import contextlib
 from typing import Callable, Optional, Sequence
 
 import torch
-from torch.func import functional_call
 
 
 def _frozen_hyperparameters(optimizer: torch.optim.Optimizer):
     """Per parameter group: every non-tensor hyperparameter (a graph replay uses the value captured)."""
     return [{k: v for k, v in g.items() if k != "params" and not torch.is_tensor(v)} for g in optimizer.param_groups]
+
+
+@contextlib.contextmanager
+def _swapped_parameters(model: torch.nn.Module, aliases):
+    """model's parameters replaced by `aliases` (name -> tensor) in their modules' _parameters, restored on exit;
+    a parameter registered under several names gets its alias everywhere"""
+    by_id = {id(p): aliases[n] for n, p in model.named_parameters() if n in aliases}
+    saved = []
+    try:
+        for mod in model.modules():
+            for k, p in list(mod._parameters.items()):
+                if p is not None and id(p) in by_id:
+                    saved.append((mod, k, p))
+                    mod._parameters[k] = by_id[id(p)]
+        yield
+    finally:
+        for mod, k, p in reversed(saved):
+            mod._parameters[k] = p
 
 
 class GraphedTrainStep:
@@ -103,9 +122,10 @@ class GraphedTrainStep:
                 t.zero_()
 
     def _body(self) -> torch.Tensor:
-        loss = self.criterion(functional_call(self.model, self.leaves, (self.x,)), self.t)
-        # autograd.grad over the aliases, not backward(): see the module docstring
-        grads = torch.autograd.grad(loss, list(self.leaves.values()), allow_unused=True)
+        with _swapped_parameters(self.model, self.leaves):
+            loss = self.criterion(self.model(self.x), self.t)
+            # autograd.grad over the aliases, not backward(): see the module docstring
+            grads = torch.autograd.grad(loss, list(self.leaves.values()), allow_unused=True)
         for p, g in zip(self.params, grads):
             p.grad = g
         if self.clip_norm is not None:
