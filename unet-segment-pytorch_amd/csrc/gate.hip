@@ -125,7 +125,8 @@ __device__ __forceinline__ void load8(const T* p, float* v) {
   }
 }
 
-constexpr int GV_U = 4;    // pixels per lane per trip of the vectorised gate passes (loads in flight)
+constexpr int GV_U = 4;    // pixels per lane per trip of the vectorised psi pass (loads in flight)
+constexpr int GV_U2 = 2;   // the same for gate passes 2 / 3 (4 measured slower there: 162 VGPRs, 28.4 -> 30.5 us)
 
 template <typename T>
 __global__ void psi_vec_kernel(long long P, int Ci, int G, const T* __restrict__ gw, const T* __restrict__ xw,
@@ -368,11 +369,11 @@ __global__ __launch_bounds__(256) void gate_bwd2_vec_kernel(long long P, int Ci,
   float a0[8], a1[8], a2[8], a3[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { a0[j] = 0.f; a1[j] = 0.f; a2[j] = 0.f; a3[j] = 0.f; }
-  // GV_U pixels per trip, loads first, summed in the one-pixel loop's order (bit-identical sums)
-  for (long long q = p0 + tid / G; q < p1; q += GV_U * slots) {
-    float g[GV_U][8], x[GV_U][8], dqv[GV_U], ppv[GV_U];
+  // GV_U2 pixels per trip, loads first, summed in the one-pixel loop's order (bit-identical sums)
+  for (long long q = p0 + tid / G; q < p1; q += GV_U2 * slots) {
+    float g[GV_U2][8], x[GV_U2][8], dqv[GV_U2], ppv[GV_U2];
 #pragma unroll
-    for (int u = 0; u < GV_U; ++u) {
+    for (int u = 0; u < GV_U2; ++u) {
       const long long qq = q + u * slots < p1 ? q + u * slots : q;
       load8<T>(gw + qq * Ci + c0, g[u]);
       load8<T>(xw + qq * Ci + c0, x[u]);
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(256) void gate_bwd2_vec_kernel(long long P, int Ci,
       ppv[u] = pp[qq];
     }
 #pragma unroll
-    for (int u = 0; u < GV_U; ++u) {
+    for (int u = 0; u < GV_U2; ++u) {
       if (q + u * slots >= p1) break;
       const float dp = A * dqv[u] + B * ppv[u] + Cc;
 #pragma unroll
@@ -436,10 +437,10 @@ __global__ __launch_bounds__(256) void gate_bwd3_vec_kernel(long long P, int Ci,
   const float A = pc[0], B = pc[1], Cc = pc[2];
   const long long per = (P + rows - 1) / rows;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  for (long long q = p0 + tid / G; q < p1; q += GV_U * slots) {
-    float g[GV_U][8], x[GV_U][8], dqv[GV_U], ppv[GV_U];
+  for (long long q = p0 + tid / G; q < p1; q += GV_U2 * slots) {
+    float g[GV_U2][8], x[GV_U2][8], dqv[GV_U2], ppv[GV_U2];
 #pragma unroll
-    for (int u = 0; u < GV_U; ++u) {
+    for (int u = 0; u < GV_U2; ++u) {
       const long long qq = q + u * slots < p1 ? q + u * slots : q;
       load8<T>(gw + qq * Ci + c0, g[u]);
       load8<T>(xw + qq * Ci + c0, x[u]);
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(256) void gate_bwd3_vec_kernel(long long P, int Ci,
       ppv[u] = pp[qq];
     }
 #pragma unroll
-    for (int u = 0; u < GV_U; ++u) {
+    for (int u = 0; u < GV_U2; ++u) {
       const long long qq = q + u * slots;
       if (qq >= p1) break;
       float og[8], ox[8];
