@@ -1,14 +1,14 @@
-"""Aggregate rocprofv3 --pmc counter_collection.csv per kernel: python tools/pmcsum.py <dir> [name-filter]"""
-import csv, glob, sys, collections
+"""Aggregate rocprofv3 --pmc counter_collection.csv per kernel: python tools/pmcsum.py <dir> [name-regex]"""
+import csv, glob, re, sys, collections
 d = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
-rows = list(csv.DictReader(open(glob.glob(d + "/*counter_collection.csv")[0])))
+rows = list(csv.DictReader(open(glob.glob(d + "/**/*counter_collection.csv", recursive=True)[0])))
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
 dur = collections.defaultdict(dict)
 for r in rows:
     k = r["Kernel_Name"]
-    if flt not in k:
+    if flt and not re.search(flt, k):
         continue
     agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
     disp[k].add(r["Dispatch_Id"])

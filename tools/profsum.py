@@ -7,12 +7,12 @@ import csv, sys, glob, collections
 d = sys.argv[1]
 steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 25
-stats = glob.glob(d + "/*kernel_stats.csv")
+stats = glob.glob(d + "/**/*kernel_stats.csv", recursive=True)
 if stats:
     rows = [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"])) for r in csv.DictReader(open(stats[0]))]
 else:
     agg = collections.defaultdict(lambda: [0, 0.0])
-    for r in csv.DictReader(open(glob.glob(d + "/*kernel_trace.csv")[0])):
+    for r in csv.DictReader(open(glob.glob(d + "/**/*kernel_trace.csv", recursive=True)[0])):
         a = agg[r["Kernel_Name"]]
         a[0] += 1
         a[1] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
