@@ -36,23 +36,24 @@
 namespace unet {
 
 constexpr int C5_W = 32, C5_HW = 34;     // tile width, halo width (pixels)
-constexpr int C5_WM = 4, C5_WN = 2, C5_NW = 8, C5_NT = 512;
+constexpr int C5_WM = 4;                 // wave row groups of a workgroup tile
+constexpr int C5_WH = 2;                 // 32-channel halves of the block's 64 output channels
 constexpr int C5_BN = 64;                // output channels per workgroup
 constexpr int C5_CMAX = 1024;            // largest BN-activation source (scale / shift table)
 constexpr int C5_NPAD = PACK_NPAD;       // packed weight rows are padded to this (conv_common.h)
 constexpr int OM5_Y = 0, OM5_F32 = 1, OM5_BNB = 2;
 
-template <int MI, bool ACT>
+template <int MI, bool ACT, int NWV>
 struct C5Layout {
   static constexpr int TH = C5_WM * MI;
   static constexpr int HP = C5_HW * (TH + 2);       // halo pixels
   static constexpr int NS = 2 * HP;                 // 16-byte slots per chunk image
   static constexpr int NI = (NS + 63) / 64;         // DMA instructions per image
-  static constexpr int DPW = (NI + C5_NW - 1) / C5_NW;
+  static constexpr int DPW = (NI + NWV - 1) / NWV;
   static constexpr int IMG = NI * 1024;             // padded: the last instruction's tail lanes land inside
   static constexpr int NCOMP = ACT ? 2 : 3;
-  static constexpr int WIMG = 9 * C5_WN * 1024;     // weight fragments of one chunk
-  static constexpr int WPW = (9 * C5_WN + C5_NW - 1) / C5_NW;
+  static constexpr int WIMG = 9 * C5_WH * 1024;     // weight fragments of one chunk
+  static constexpr int WPW = (9 * C5_WH + NWV - 1) / NWV;
   static constexpr int OFF_COMP = 0;
   static constexpr int OFF_RAW = OFF_COMP + NCOMP * IMG;
   static constexpr int OFF_W = OFF_RAW + (ACT ? 2 * IMG : 0);
@@ -69,19 +70,24 @@ struct C5Layout {
 // gate (compile-time, so the transform is one straight-line block).  ABL (diagnostic ablations,
 // unet_diag_conv5_ablate; 0 in the product): 1 no in-loop halo DMA, 2 no in-loop weight DMA, 4 no epilogue,
 // 8 no per-chunk barrier, 16 no BN transform
-template <typename T, int MI, int OM, int SK, int GATE, int ABL = 0, int PIPE = 1>
-__global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d, int tiles_w, int tiles_h, int mtiles,
-                                                        int nch) {
+// NWV: waves per workgroup.  8 = 4 row groups x 2 channel halves (two waves per SIMD, each 32 output
+// channels); 4 = 4 row groups, each wave all 64 channels (one wave per SIMD with the whole 512-register file:
+// every halo fragment it reads from LDS feeds twice the MFMAs — 12 reads per 24 MFMAs per tap column instead
+// of 9 per 12 — and the two accumulator halves and both operand columns fit without spills)
+template <typename T, int MI, int OM, int SK, int GATE, int ABL = 0, int PIPE = 1, int NWV = 8>
+__global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc d, int tiles_w, int tiles_h,
+                                                           int mtiles, int nch) {
   using F = typename Mma32<T>::frag;
   constexpr bool ACT = SK != SK_PLAIN;
-  using Lay = C5Layout<MI, ACT>;
+  constexpr int WN = NWV / C5_WM, NJ = C5_WH / WN, NT = 64 * NWV;
+  using Lay = C5Layout<MI, ACT, NWV>;
   constexpr int TH = Lay::TH, NS = Lay::NS, NI = Lay::NI, DPW = Lay::DPW, WPW = Lay::WPW;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[Lay::BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int cw0 = blockIdx.y * C5_BN + wn * 32;     // this wave's first output channel
+  const int wm = WN == 2 ? wave >> 1 : wave, wn = WN == 2 ? (wave & 1) : 0;
+  const int cw0 = blockIdx.y * C5_BN + wn * 32;     // this wave's first output channel (NJ blocks of 32)
   const int ntl = (mtiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;   // tiles of this block
   const int G = ntl * nch;                          // chunk steps of this block
   auto tile_of = [&](int ti, int& n_, int& h0_, int& w0_) {
@@ -126,7 +132,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   int soy[DPW], sox[DPW];   // the slot's pixel offset from the tile origin (halo: -1 .. TH, -1 .. 32)
 #pragma unroll
   for (int k = 0; k < DPW; ++k) {
-    const int i = wave + k * C5_NW, s = i * 64 + lane;
+    const int i = wave + k * NWV, s = i * 64 + lane;
     const int hp = s >> 1;
     hbit[k] = (s & 1) ^ ((hp >> 3) & 1);
     soy[k] = s < NS ? hp / C5_HW - 1 : -(1 << 20);    // past the image: never a valid row
@@ -203,7 +209,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     if (!(ABL & 1) || prologue) {
 #pragma unroll
       for (int k = 0; k < DPW; ++k) {
-        const int i = wave + k * C5_NW;
+        const int i = wave + k * NWV;
         unsigned vo = (s1sel ? ib1[k] : ib0[k]) + (unsigned)cl * 2u;   // stays >= OOB when the base is
         if (rag && hbit[k]) vo = OOB;
         dma16(rs, i < NI ? img + i * 1024 : junk, vo);
@@ -214,11 +220,11 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       const unsigned wofs = (unsigned)((q.c >> 1) * 9) * 1024u + (unsigned)(q.c & 1) * 512u;
 #pragma unroll
       for (int k = 0; k < WPW; ++k) {
-        const int j = wave + k * C5_NW;
+        const int j = wave + k * NWV;
         const int tap = j >> 1, wj = j & 1;
         const unsigned nt0 = (unsigned)((blockIdx.y * C5_BN + wj * 32) / 16);
         const unsigned vo = lanew + nt0 * jstride + (unsigned)tap * 1024u + wofs;
-        dma16(rw, j < 9 * C5_WN ? wd + j * 1024 : junk, j < 9 * C5_WN ? vo : OOB);
+        dma16(rw, j < 9 * C5_WH ? wd + j * 1024 : junk, j < 9 * C5_WH ? vo : OOB);
       }
     }
     const bool gl = gated && q.c == 0;
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       const unsigned pbase = ((unsigned)q.n * d.H + q.h0) * d.W + q.w0;
 #pragma unroll
       for (int k = 0; k < DPW; ++k) {
-        const int i = wave + k * C5_NW;
+        const int i = wave + k * NWV;
         const unsigned pix = pbase + (unsigned)(soy[k] * d.W + sox[k]);
         dma4(rsg, i < NI ? gd + i * 256 : junk, ib0[k] < OOB ? pix * 4u : OOB);
       }
@@ -268,7 +274,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     const float* tab = reinterpret_cast<const float*>(lds + Lay::OFF_TAB);
 #pragma unroll
     for (int k = 0; k < DPW; ++k) {
-      const int i = wave + k * C5_NW;
+      const int i = wave + k * NWV;
       const bool live = i < NI;                      // slots past the image: the junk region (no branch)
       const int s = i * 64 + lane;
       const unsigned so = live ? (unsigned)s * 16u : (unsigned)(Lay::OFF_JUNK + lane * 16);
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
   // ---- prologue: scale/shift table, chunks 0-2 in flight, chunk 0 ready ----
   if constexpr (ACT) {
     float* tab = reinterpret_cast<float*>(lds + Lay::OFF_TAB);
-    for (int c = tid; c < C0; c += C5_NT) { tab[c] = s0.scale[c]; tab[C5_CMAX + c] = s0.shift[c]; }
+    for (int c = tid; c < C0; c += NT) { tab[c] = s0.scale[c]; tab[C5_CMAX + c] = s0.shift[c]; }
     if (tid < 8) { tab[C0 + tid] = 0.f; tab[C5_CMAX + C0 + tid] = 0.f; }
   }
   if constexpr (OM == OM5_BNB) {
@@ -356,38 +362,44 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
 
   // BatchNorm sums of this lane's pixel column over the block's tiles (reduced once, after the last tile)
   constexpr bool SUMS = OM == OM5_Y || OM == OM5_BNB;
-  float sA[16], sB[16];
+  float sA[NJ][16], sB[NJ][16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { sA[r] = 0.f; sB[r] = 0.f; }
-  f32x16 acc[MI];
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { sA[j][r] = 0.f; sB[j][r] = 0.f; }
+  f32x16 acc[MI][NJ];
 
   // operand fragments of one tap column dx of the chunk at K: MI+2 halo rows (B) and the 3 taps' weights (A)
-  auto load_col = [&](const Cur& q, int dx, F (&x)[MI + 2], F (&w)[3]) {
+  auto load_col = [&](const Cur& q, int dx, F (&x)[MI + 2], F (&w)[3][NJ]) {
     const unsigned char* xb = comp_buf(ACT ? q.s2 : q.s3);
-    const unsigned char* wb = w_buf(q.s3) + wn * 1024 + lane * 16;
+    const unsigned char* wb = w_buf(q.s3) + wn * NJ * 1024 + lane * 16;
 #pragma unroll
     for (int rr = 0; rr < MI + 2; ++rr) x[rr] = *reinterpret_cast<const F*>(xb + xoff[dx][rr]);
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) w[dy] = *reinterpret_cast<const F*>(wb + (dy * 3 + dx) * 2048);
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) w[dy][j] = *reinterpret_cast<const F*>(wb + j * 1024 + (dy * 3 + dx) * 2048);
   };
-  auto mma_col = [&](const F (&x)[MI + 2], const F (&w)[3]) {
+  auto mma_col = [&](const F (&x)[MI + 2], const F (&w)[3][NJ]) {
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-      for (int i = 0; i < MI; ++i) acc[i] = Mma32<T>::mma(w[dy], x[i + dy], acc[i]);
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < MI; ++i) acc[i][j] = Mma32<T>::mma(w[dy][j], x[i + dy], acc[i][j]);
   };
   // this wave's DMAs of the chunk after K have landed: only the youngest chunk's may still be in flight
   // (the y epilogue's NST stores sit between DMA batches for the two chunks after it: sw counts them down)
   // (BNB: the epilogue's 4 MI 8-byte g stores likewise; and the tile's NYL y1 loads, issued at the start of
   // its last chunk — after the two in-flight DMA batches — are counted by that chunk's wait: yl)
-  constexpr int NST = OM == OM5_Y ? 2 * MI : (OM == OM5_BNB || OM == OM5_F32 ? 4 * MI : 0);
+  constexpr int NST = NJ * (OM == OM5_Y ? 2 * MI : (OM == OM5_BNB || OM == OM5_F32 ? 4 * MI : 0));
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
   // F32 without accumulation: counted buffer stores (no RMW loads, whose compiler waits drain the DMA queue)
   const bool f32_counted = OM == OM5_F32 && !d.accum && !d.accum2 && (d.split % 8) == 0 &&
                            (double)npix * d.Cout * 4 < (double)OOB;
   const rsrc_t rf1 = mk_rsrc(d.out, (unsigned)(f32_counted ? npix * d.split * 4 : 0));
   const rsrc_t rf2 = mk_rsrc(d.out2 ? d.out2 : d.out, (unsigned)(f32_counted ? npix * (d.Cout - d.split) * 4 : 0));
-  constexpr int NYL = OM == OM5_BNB ? 4 * MI : 0;
+  constexpr int NYL = OM == OM5_BNB ? 4 * MI * NJ : 0;
   int sw = 0;
   auto wait_next = [&](bool yl) {
     const bool st = NST && sw > 0;
@@ -420,26 +432,27 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     }
   };
 
-  F xA[MI + 2], wA[3], xB[MI + 2], wB[3];
+  F xA[MI + 2], wA[3][NJ], xB[MI + 2], wB[3][NJ];
   // PIPE 1: the operands of tap column dx+1 are read from LDS while the MFMAs of column dx run (pinned
   // one ds_read per MFMA by sched_group_barrier), and column 0 of the next chunk right after the barrier.
   // hipcc's own schedule (PIPE 0) reads every fragment just before its MFMA with an lgkmcnt(0) in between;
   // PIPE 1 measured 5-9 % faster per layer for the y / fp32 epilogues (launch5)
   auto pin_col = [&]() {
     if constexpr (PIPE) {
+      constexpr int NDS = MI + 2 + 3 * NJ, NMF = 3 * MI * NJ;   // reads of the next column, MFMAs of this one
 #pragma unroll
-      for (int i = 0; i < MI + 5; ++i) {
+      for (int i = 0; i < NDS; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 3 * MI - (MI + 5), 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF - NDS, 0);
     }
   };
   if constexpr (PIPE) load_col(K, 0, xA, wA);
   // BNB: the activation y1 of this wave's tile pixels (buffer loads, out-of-range offsets for masked lanes:
   // a fixed count), loaded during the tile's last chunk so that the epilogue's wait for them does not drain
   // the next chunks' DMAs (their issue follows the epilogue)
-  uint2 yv[OM == OM5_BNB ? MI : 1][4];
+  uint2 yv[OM == OM5_BNB ? MI : 1][NJ][4];
   const rsrc_t ry1 = mk_rsrc(OM == OM5_BNB ? d.bnb_y : d.out, (unsigned)(npix * d.Cout * 2));
   auto load_y1 = [&](int ti) {
     int n, h0, w0;
@@ -449,18 +462,22 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
 #pragma unroll
     for (int i = 0; i < (OM == OM5_BNB ? MI : 0); ++i)
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int co = cw0 + 8 * gq + 4 * (lane >> 5);
-        const bool ok = ow < d.W && oh0 + i < d.H && co < d.Cout;
-        const unsigned vo = ok ? ((pix0 + (unsigned)i * d.W) * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
-        yv[i][gq] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ry1, (int)vo, 0, 0));
-      }
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int co = cw0 + 32 * j + 8 * gq + 4 * (lane >> 5);
+          const bool ok = ow < d.W && oh0 + i < d.H && co < d.Cout;
+          const unsigned vo = ok ? ((pix0 + (unsigned)i * d.W) * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
+          yv[i][j][gq] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ry1, (int)vo, 0, 0));
+        }
   };
   for (int ti = 0; ti < ntl; ++ti) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 #pragma unroll 1
     for (int c = 0; c < nch; ++c) {
       // one tap column at a time; the barrier ends the chunk (after it: chunk K's slots are free and the
@@ -502,7 +519,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     if constexpr (ABL & 4) {
       float sum = 0.f;
 #pragma unroll
-      for (int i = 0; i < MI; ++i) sum += acc[i][0] + acc[i][7] + acc[i][15];
+      for (int i = 0; i < MI; ++i) sum += acc[i][0][0] + acc[i][NJ - 1][7] + acc[i][0][15];
       if (sum == 12345.f) ((float*)d.out)[tid] = sum;
       continue;
     }
@@ -517,6 +534,8 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     const unsigned pix0 = ((unsigned)n * d.H + oh0) * (unsigned)d.W + ow;
     if constexpr (OM == OM5_Y) {
 #pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
       for (int i = 0; i < MI; ++i) {
         const bool ok = colok && i < rows;
         const unsigned pix = pix0 + (unsigned)i * d.W;
@@ -528,14 +547,14 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
         unsigned px_[4], py_[4];
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          px_[gq] = pack2_16<T>(acc[i][4 * gq], acc[i][4 * gq + 1]);
-          py_[gq] = pack2_16<T>(acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
+          px_[gq] = pack2_16<T>(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
+          py_[gq] = pack2_16<T>(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
         }
 #pragma unroll
         for (int kp = 0; kp < 4; kp += 2) {
           const auto sx = __builtin_amdgcn_permlane32_swap(px_[kp], px_[kp + 1], false, false);
           const auto sy = __builtin_amdgcn_permlane32_swap(py_[kp], py_[kp + 1], false, false);
-          const int co = cw0 + 8 * kp + 8 * hh;
+          const int co = cw0 + 32 * j + 8 * kp + 8 * hh;
           const unsigned vo = (ok && co < d.Cout) ? (pix * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
           typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
           const u32x4 v4 = {sx[0], sy[0], sx[1], sy[1]};
@@ -545,13 +564,15 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       sw = 2;
       if (d.stats) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
-          for (int i = 0; i < MI; ++i) {
-            const float x = (colok && i < rows) ? acc[i][r] : 0.f;
-            sA[r] += x;
-            sB[r] = __builtin_fmaf(x, x, sB[r]);
-          }
+          for (int r = 0; r < 16; ++r)
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+              const float x = (colok && i < rows) ? acc[i][j][r] : 0.f;
+              sA[j][r] += x;
+              sB[j][r] = __builtin_fmaf(x, x, sB[j][r]);
+            }
       }
     } else if constexpr (OM == OM5_BNB) {
       // g stored as buffer stores (fixed count NST, out-of-range offsets mask lanes); the BN affine of the
@@ -559,8 +580,10 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       const float* btab = reinterpret_cast<const float*>(lds + Lay::OFF_BTAB);
       const rsrc_t rg = mk_rsrc(d.out, (unsigned)(npix * d.Cout * 2));
 #pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
-        const int co = cw0 + 8 * gq + 4 * hh;
+        const int co = cw0 + 32 * j + 8 * gq + 4 * hh;
         const bool cok = co < d.Cout;
         const int cb = co - (int)blockIdx.y * C5_BN;
         const float4 a4 = *reinterpret_cast<const float4*>(btab + cb);
@@ -571,20 +594,20 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
           const unsigned pix = pix0 + (unsigned)i * d.W;
           const bool ok = colok && i < rows && cok;
           uint2 pk;
-          pk.x = pack2_16<T>(acc[i][4 * gq], acc[i][4 * gq + 1]);
-          pk.y = pack2_16<T>(acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
+          pk.x = pack2_16<T>(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
+          pk.y = pack2_16<T>(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
           const unsigned vo = ok ? (pix * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
           typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), rg, (int)vo, 0, 0);
           if (ok) {
             float gv[4], yy[4];
             unpack4_16<T>(pk, gv);
-            unpack4_16<T>(yv[i][gq], yy);
+            unpack4_16<T>(yv[i][j][gq], yy);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float gg = (d.bnb_relu && !(yy[r] * sc4[r] + sf4[r] > 0.f)) ? 0.f : gv[r];
-              sA[4 * gq + r] += gg;
-              sB[4 * gq + r] = __builtin_fmaf(gg, yy[r], sB[4 * gq + r]);
+              sA[j][4 * gq + r] += gg;
+              sB[j][4 * gq + r] = __builtin_fmaf(gg, yy[r], sB[j][4 * gq + r]);
             }
           }
         }
@@ -594,17 +617,19 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     } else if (f32_counted) {  // OM5_F32, plain stores: buffer stores, fixed count NST (sw as the y epilogue)
       const int c2 = d.Cout - d.split;
 #pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
       for (int i = 0; i < MI; ++i) {
         const unsigned pix = pix0 + (unsigned)i * d.W;
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          const int co = cw0 + 8 * gq + 4 * hh;
-          const bool to1 = cw0 + 8 * gq < d.split;     // wave-uniform (split % 8 == 0)
+          const int co = cw0 + 32 * j + 8 * gq + 4 * hh;
+          const bool to1 = cw0 + 32 * j + 8 * gq < d.split;     // wave-uniform (split % 8 == 0)
           const bool ok = colok && i < rows && co < d.Cout;
           const unsigned vo = !ok ? OOB : to1 ? (pix * (unsigned)d.split + (unsigned)co) * 4u
                                              : (pix * (unsigned)c2 + (unsigned)(co - d.split)) * 4u;
           typedef __attribute__((ext_vector_type(4))) float f32x4v;
-          const f32x4v w = {acc[i][4 * gq], acc[i][4 * gq + 1], acc[i][4 * gq + 2], acc[i][4 * gq + 3]};
+          const f32x4v w = {acc[i][j][4 * gq], acc[i][j][4 * gq + 1], acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]};
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, w), to1 ? rf1 : rf2, (int)vo, 0, 0);
         }
       }
@@ -614,6 +639,8 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       float* o2 = (float*)d.out2;
       const int c2 = d.Cout - d.split;
 #pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
       for (int i = 0; i < MI; ++i) {
         if (!(colok && i < rows)) continue;
         const unsigned pix = pix0 + (unsigned)i * d.W;
@@ -622,7 +649,7 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
         bool acc_in[4];
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          const int co = cw0 + 8 * gq + 4 * hh;
+          const int co = cw0 + 32 * j + 8 * gq + 4 * hh;
           if (co < d.split) {
             pp[gq] = reinterpret_cast<float4*>(o1 + (size_t)pix * d.split + co);
             acc_in[gq] = d.accum;
@@ -635,9 +662,9 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
         }
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
-          const int co = cw0 + 8 * gq + 4 * hh;
+          const int co = cw0 + 32 * j + 8 * gq + 4 * hh;
           if (co < d.Cout) {
-            float4 w = make_float4(acc[i][4 * gq], acc[i][4 * gq + 1], acc[i][4 * gq + 2], acc[i][4 * gq + 3]);
+            float4 w = make_float4(acc[i][j][4 * gq], acc[i][j][4 * gq + 1], acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
             if (acc_in[gq]) { w.x += old[gq].x; w.y += old[gq].y; w.z += old[gq].z; w.w += old[gq].w; }
             *pp[gq] = w;
           }
@@ -653,9 +680,11 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
     if constexpr (OM == OM5_Y) {
       if (d.stats) {
 #pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float a = half32_sum(sA[r]), b = half32_sum(sB[r]);
-          const int co = cw0 + 8 * (r >> 2) + 4 * hh + (r & 3);
+          const float a = half32_sum(sA[j][r]), b = half32_sum(sB[j][r]);
+          const int co = cw0 + 32 * j + 8 * (r >> 2) + 4 * hh + (r & 3);
           if ((lane & 31) == 0 && co < d.Cout) {
             d.stats[(size_t)co * srows + srow] = a;
             d.stats[((size_t)d.Cout + co) * srows + srow] = b;
@@ -664,13 +693,15 @@ __global__ __launch_bounds__(C5_NT, 1) void conv5_kernel(const unet_conv_desc d,
       }
     } else {
 #pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
-        const int co = cw0 + 8 * gq + 4 * hh;
+        const int co = cw0 + 32 * j + 8 * gq + 4 * hh;
         float a[4], b[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          a[r] = half32_sum(sA[4 * gq + r]);
-          b[r] = half32_sum(sB[4 * gq + r]);
+          a[r] = half32_sum(sA[j][4 * gq + r]);
+          b[r] = half32_sum(sB[j][4 * gq + r]);
         }
         if ((lane & 31) == 0 && co < d.Cout) {
           const float4 m4 = *reinterpret_cast<const float4*>(d.bnb_mean + co);
@@ -760,6 +791,12 @@ int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
 // the 512^2 64->64 forward, profiles/r04_layerprof_conv5_pipe{0,1}.txt); the BN-backward-sums epilogue keeps
 // the compiler's schedule: with both operand columns and its 16 y1 registers live it ran out of VGPRs
 // (256 + 108 bytes of scratch) and went 14-30 % slower
+// UNET_CONV5_WAVES=4: the one-wave-per-SIMD form (NWV 4, 64 channels per wave), else the 8-wave form
+static int conv5_waves() {
+  const char* e = getenv("UNET_CONV5_WAVES");
+  return e && atoi(e) == 4 ? 4 : 8;
+}
+
 template <typename T, int OM, int SK, int GATE, int ABL = 0>
 static int launch5(const unet_conv_desc* d, hipStream_t st) {
   constexpr int TH = C5_WM * C5_MI;
@@ -768,8 +805,12 @@ static int launch5(const unet_conv_desc* d, hipStream_t st) {
   const int mt = d->N * tw * th;
   const int gy = cdiv(d->Cout, C5_BN);
   const int gx = conv5_gx(d);
-  hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, PIPE>), dim3(gx, gy), dim3(C5_NT), 0, st, *d, tw, th,
-                     mt, cdiv(d->Cin, 16));
+  if (conv5_waves() == 4)
+    hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, 1, 4>), dim3(gx, gy), dim3(256), 0, st, *d, tw, th,
+                       mt, cdiv(d->Cin, 16));
+  else
+    hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, PIPE, 8>), dim3(gx, gy), dim3(512), 0, st, *d, tw,
+                       th, mt, cdiv(d->Cin, 16));
   return check_launch("conv5");
 }
 
