@@ -148,6 +148,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
     for (int rr = 0; rr < MI + 2; ++rr) {
       const int hp = (wm * MI + rr) * C5_HW + (lane & 31) + dx;
       xoff[dx][rr] = (unsigned)(2 * hp + ((lane >> 5) ^ ((hp >> 3) & 1))) * 16u;
+      // opaque to the optimiser: otherwise it splits each offset into two registers and spends two VALU
+      // (v_or + v_add) per B-fragment read instead of one v_add of the ring slot's base
+      asm volatile("" : "+v"(xoff[dx][rr]));
     }
 
   // ring slots: compute images (PLAIN: 3 = chunk % 3; ACT: 2 = chunk & 1), raw images (ACT: chunk & 1),
@@ -563,16 +566,34 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
       }
       sw = 2;
       if (d.stats) {
+        // channel pairs on v_pk_add_f32 / v_pk_fma_f32 (each element's sum in the same order); the masks only
+        // on a tile that crosses the map's bottom or right edge (wave-uniform)
+        typedef __attribute__((ext_vector_type(2))) float f2s;
+        const bool full = rows == MI && w0 + C5_W <= d.W;
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
+          for (int r = 0; r < 16; r += 2) {
+            f2s a2 = {sA[j][r], sA[j][r + 1]}, b2 = {sB[j][r], sB[j][r + 1]};
+            if (full) {
 #pragma unroll
-            for (int i = 0; i < MI; ++i) {
-              const float x = (colok && i < rows) ? acc[i][j][r] : 0.f;
-              sA[j][r] += x;
-              sB[j][r] = __builtin_fmaf(x, x, sB[j][r]);
+              for (int i = 0; i < MI; ++i) {
+                const f2s x2 = {acc[i][j][r], acc[i][j][r + 1]};
+                a2 += x2;
+                b2 = __builtin_elementwise_fma(x2, x2, b2);
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < MI; ++i) {
+                const bool ok = colok && i < rows;
+                const f2s x2 = {ok ? acc[i][j][r] : 0.f, ok ? acc[i][j][r + 1] : 0.f};
+                a2 += x2;
+                b2 = __builtin_elementwise_fma(x2, x2, b2);
+              }
             }
+            sA[j][r] = a2.x; sA[j][r + 1] = a2.y;
+            sB[j][r] = b2.x; sB[j][r + 1] = b2.y;
+          }
       }
     } else if constexpr (OM == OM5_BNB) {
       // g stored as buffer stores (fixed count NST, out-of-range offsets mask lanes); the BN affine of the
