@@ -812,12 +812,9 @@ int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
 // the 512^2 64->64 forward, profiles/r04_layerprof_conv5_pipe{0,1}.txt); the BN-backward-sums epilogue keeps
 // the compiler's schedule: with both operand columns and its 16 y1 registers live it ran out of VGPRs
 // (256 + 108 bytes of scratch) and went 14-30 % slower
-// UNET_CONV5_WAVES=4: the one-wave-per-SIMD form (NWV 4, 64 channels per wave), else the 8-wave form
-static int conv5_waves() {
-  const char* e = getenv("UNET_CONV5_WAVES");
-  return e && atoi(e) == 4 ? 4 : 8;
-}
-
+// The 8-wave form (NWV 8).  The one-wave-per-SIMD form (NWV 4: 64 channels per wave, 12 LDS reads per 24 MFMAs
+// per tap column, 462-502 registers, no spills) measured 10-25 % slower on every layer
+// (profiles/r04_layerprof_conv5_{8,4}waves.txt): one wave cannot cover its own LDS and DMA latencies.
 template <typename T, int OM, int SK, int GATE, int ABL = 0>
 static int launch5(const unet_conv_desc* d, hipStream_t st) {
   constexpr int TH = C5_WM * C5_MI;
@@ -826,12 +823,8 @@ static int launch5(const unet_conv_desc* d, hipStream_t st) {
   const int mt = d->N * tw * th;
   const int gy = cdiv(d->Cout, C5_BN);
   const int gx = conv5_gx(d);
-  if (conv5_waves() == 4)
-    hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, 1, 4>), dim3(gx, gy), dim3(256), 0, st, *d, tw, th,
-                       mt, cdiv(d->Cin, 16));
-  else
-    hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, PIPE, 8>), dim3(gx, gy), dim3(512), 0, st, *d, tw,
-                       th, mt, cdiv(d->Cin, 16));
+  hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, PIPE, 8>), dim3(gx, gy), dim3(512), 0, st, *d, tw, th,
+                     mt, cdiv(d->Cin, 16));
   return check_launch("conv5");
 }
 
@@ -842,7 +835,9 @@ static int dispatch5_om(const unet_conv_desc* d, hipStream_t st) {
   const unet_src& s0 = d->src[0];
   if (s0.kind != UNET_SRC_ACT) return launch5<T, OM, SK_PLAIN, 0>(d, st);
   const bool g = s0.gate_p != nullptr;
-  if (OM == OM5_Y && d->nsrc == 1) return g ? launch5<T, OM, SK_ACT, 1>(d, st) : launch5<T, OM, SK_ACT, 0>(d, st);
+  if constexpr (OM == OM5_Y) {
+    if (d->nsrc == 1) return g ? launch5<T, OM, SK_ACT, 1>(d, st) : launch5<T, OM, SK_ACT, 0>(d, st);
+  }
   return g ? launch5<T, OM, SK_ACT_PLAIN, 1>(d, st) : launch5<T, OM, SK_ACT_PLAIN, 0>(d, st);
 }
 
