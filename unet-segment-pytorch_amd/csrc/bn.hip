@@ -192,6 +192,41 @@ __device__ __forceinline__ void pool_add8(const PoolG& pg, int C, long long p, i
   }
 }
 
+// a pixel's (n, h, w), advanced in place by a fixed pixel step (no per-pixel division): the routed pooled
+// gradient of a thread's pixel sequence p, p + S, p + 2S, ...
+struct PixCur {
+  unsigned n, h, w;
+};
+__device__ __forceinline__ PixCur pix_cur(const PoolG& pg, unsigned p) {
+  const unsigned W = (unsigned)pg.W, H = (unsigned)pg.H;
+  const unsigned t = p / W, w = p - t * W;
+  const unsigned n = t / H;
+  return PixCur{n, t - n * H, w};
+}
+// step = sq * W + sr (sr < W), split once by the caller
+__device__ __forceinline__ void pix_adv(PixCur& c, const PoolG& pg, unsigned sq, unsigned sr) {
+  c.w += sr;
+  unsigned h = c.h + sq;
+  if (c.w >= (unsigned)pg.W) { c.w -= (unsigned)pg.W; ++h; }
+  while (h >= (unsigned)pg.H) { h -= (unsigned)pg.H; ++c.n; }
+  c.h = h;
+}
+__device__ __forceinline__ void pool_add8c(const PoolG& pg, int C, const PixCur& pc, int c0, float* g) {
+  const unsigned hh = pc.h >> 1, ww = pc.w >> 1;
+  if (hh >= (unsigned)pg.ph || ww >= (unsigned)pg.pw) return;
+  const size_t o = (size_t)((pc.n * (unsigned)pg.ph + hh) * (unsigned)pg.pw + ww) * C + c0;
+  const uint2 cw = *reinterpret_cast<const uint2*>(pg.code + o);
+  const float4 a = *reinterpret_cast<const float4*>(pg.g2 + o);
+  const float4 b = *reinterpret_cast<const float4*>(pg.g2 + o + 4);
+  const unsigned q = (pc.h & 1) * 2 + (pc.w & 1);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned cj = ((j < 4 ? cw.x : cw.y) >> (8 * (j & 3))) & 0xffu;
+    if (cj == q) g[j] += v[j];
+  }
+}
+
 // vectorised forms (C % 8 == 0): a thread owns 8 channels (16-byte y, 2 x 16-byte da) of one pixel;
 // the block covers 256 / (C/8) pixels per iteration with a fixed channel vector per thread.
 // POOL: + the pooled gradient (PoolG); da may then be null (no other consumer)
@@ -214,8 +249,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int
     sg[j] = 0.f; sgx[j] = 0.f;
   }
   // 4 pixels per trip without the pooled gradient (17.6 -> 15.7 us per launch); with it the extra registers
-  // cost more than the overlap gains (59 -> 64 us), so one
+  // cost more than the overlap gains (59 -> 64 us), so one.  The pooled gradient's pixel coordinates advance
+  // by the fixed step R (pix_adv) instead of two 32-bit divisions per pixel
   constexpr int BNR_U = POOL ? 1 : 4;
+  PixCur pc{0, 0, 0};
+  const unsigned sq = POOL ? (unsigned)R / (unsigned)(pg.W > 0 ? pg.W : 1) : 0u, sr = POOL ? (unsigned)R - sq * (unsigned)pg.W : 0u;
+  if (POOL && py < R && p0 + py < p1) pc = pix_cur(pg, (unsigned)(p0 + py));
   if (py < R) {
     // BNR_U pixels per trip, all their loads issued before the sums (one memory round trip per trip, not
     // per pixel); the sums still run over p, p + R, p + 2R, ... in order (bit-identical to one per trip)
@@ -234,7 +273,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int
 #pragma unroll
           for (int j = 0; j < 8; ++j) g[u][j] = 0.f;
         }
-        if constexpr (POOL) pool_add8(pg, C, q, cv * 8, g[u]);
+        if constexpr (POOL) {
+          pool_add8c(pg, C, pc, cv * 8, g[u]);
+          pix_adv(pc, pg, sq, sr);
+        }
       }
 #pragma unroll
       for (int u = 0; u < BNR_U; ++u) {
@@ -280,28 +322,44 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int 
     sc[j] = scale[c]; sf[j] = shift[c]; A[j] = coef[c]; B[j] = coef[C + c]; Cc[j] = coef[2 * C + c];
   }
   const int cvs = __builtin_ctz(CV);  // CV is a power of two (bn_vec_ok)
-  for (; e < total; e += stride) {
-    const long long p = e >> cvs;
-    float yv[8], g[8], o[8];
-    load_vec<T>(y + p * C + cv * 8, yv);
-    if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
-    if (!POOL || da) {
-      load8<G>(da + p * C + cv * 8, g);
-    } else {
+  // 2 pixels per trip, every load issued before the stores (dy may alias the loads as far as the compiler
+  // knows, which serialised one memory round trip per pixel); elementwise, so the results are unchanged
+  constexpr int U = 2;
+  for (; e < total; e += U * stride) {
+    float yv[U][8], g[U][8];
+    long long pu[U];
+    bool ok[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = 0.f;
-    }
-    if constexpr (POOL) pool_add8(pg, C, p, cv * 8, g);
+    for (int u = 0; u < U; ++u) {
+      ok[u] = e + u * stride < total;
+      pu[u] = (ok[u] ? e + u * stride : e) >> cvs;
+      const long long p = pu[u];
+      load_vec<T>(y + p * C + cv * 8, yv[u]);
+      if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv[u] + 4);
+      if (!POOL || da) {
+        load8<G>(da + p * C + cv * 8, g[u]);
+      } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[j];
-      o[j] = A[j] * gj + B[j] * yv[j] + Cc[j];
+        for (int j = 0; j < 8; ++j) g[u][j] = 0.f;
+      }
+      if constexpr (POOL) pool_add8(pg, C, p, cv * 8, g[u]);
     }
-    if constexpr (sizeof(T) == 2) {
-      store_vec<T>(dy + p * C + cv * 8, o);
-    } else {
-      store_vec<T>(dy + p * C + cv * 8, o);
-      store_vec<T>(dy + p * C + cv * 8 + 4, o + 4);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) break;
+      const long long p = pu[u];
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gj = (relu && !(yv[u][j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[u][j];
+        o[j] = A[j] * gj + B[j] * yv[u][j] + Cc[j];
+      }
+      if constexpr (sizeof(T) == 2) {
+        store_vec<T>(dy + p * C + cv * 8, o);
+      } else {
+        store_vec<T>(dy + p * C + cv * 8, o);
+        store_vec<T>(dy + p * C + cv * 8 + 4, o + 4);
+      }
     }
   }
 }
