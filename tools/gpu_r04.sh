@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU evidence, one parameterised script (replaces round 3's one-off gpu_r03*.sh files).
-#   TAG=<dir under gpurun_out>  STEPS="tests smoke bench c5 c2 trace layerprof pmc hbmpmc sq repro"  bash tools/gpu_r04.sh
+#   TAG=<dir under gpurun_out>  STEPS="tests smoke bench c5 c2 trace layerprof pmc sq ablate ab lp gdiag repro"  bash tools/gpu_r04.sh
 # Every GPU step runs under its own time limit; the chain stops at the first failure (no retries).
 set -o pipefail
 O=gpurun_out/${TAG:-r04}
@@ -59,6 +59,13 @@ for step in ${STEPS:-tests smoke bench}; do
     for v in "${ABA:-}" "${ABB:-}" ${ABC:+"$ABC"} "${ABA:-}"; do
       env $v timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-fp32-line --no-graph-line > $O/ab.json 2> $O/ab.err || fail "ab bench $v" $O/ab.err
       echo "[$v] $(python -c "import json;d=json.load(open('$O/ab.json'));print(d['value'],d['ms_per_step'],d['roofline']['avg_us'])")"
+    done ;;
+  lp)      # layer timing under several environment settings (LPS: ';'-separated), summary lines matching LPGREP
+    IFS=';' read -ra cfgs <<< "${LPS:-}"
+    for v in "${cfgs[@]}"; do
+      f="$O/lp_${v//[^A-Za-z0-9]/_}.txt"
+      env $v timeout -k 10 300 python -u tools/layerprof.py > "$f" 2>&1 || fail "lp $v" "$f"
+      echo "[$v]"; grep -E "${LPGREP:-total}" "$f" | head -${LPN:-20}
     done ;;
   gdiag)
     timeout -k 10 180 python -u tools/graphed_diag.py > $O/graphed_diag.log 2>&1 || fail gdiag $O/graphed_diag.log 40

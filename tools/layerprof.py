@@ -1,8 +1,8 @@
 """Per-launch timing of one full training step (every C-ABI call bracketed by HIP events).
 
 usage: python tools/layerprof.py [--model attention_unet|unet] [--batch 4] [--size 512] [--prec bf16]
-Prints one line per conv fwd / dgrad / wgrad launch (geometry, source kinds, variant, us, TFLOP/s)
-and a per-entry-point summary.  Diagnostic only (not part of the product or the tests)."""
+Prints one line per conv fwd / dgrad / wgrad launch (geometry, source kinds, variant, us, TFLOP/s), one
+per HBM-bound launch of the bench line's hbm block (algorithmic bytes, GB/s) and a per-entry-point summary.  Diagnostic only (not part of the product or the tests)."""
 import argparse
 import collections
 import sys
@@ -15,6 +15,9 @@ import torch  # noqa: E402
 
 from unet._hip import lib as L  # noqa: E402
 from unet._hip.runtime import conv_kernel_name, wgrad_kernel_name  # noqa: E402
+
+sys.path.insert(0, str(ROOT))
+from bench import _hbm_bytes  # noqa: E402  (the algorithmic bytes of the bench line's hbm block)
 
 KIND = {0: "plain", 1: "act", 2: "pool", 3: "up", 4: "nchw", 5: "upplain"}
 OUT = {0: "y", 1: "f32", 2: "poolbwd", 3: "shuf2", 4: "f32gate"}
@@ -40,6 +43,12 @@ def _call(name, *args):
     if not _on[0]:
         return _orig(name, *args)
     info, fl = (_desc_info(name, args[0]) if name in ("unet_conv", "unet_conv_wgrad") else (name, 0.0))
+    hb = _hbm_bytes(name, args)
+    if hb is not None and name not in ("unet_conv", "unet_conv_wgrad"):
+        info = f"{name} {hb[1] / 1e6:.1f} MB"
+        fl = -hb[1]          # negative: algorithmic bytes (HBM-bound line)
+    elif hb is not None:
+        info += f" | {hb[1] / 1e6:.1f} MB"
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     r = _orig(name, *args)
@@ -87,8 +96,10 @@ def main():
     for key, name, fl in order:
         us = min(per[key])
         tot[name] += us
-        if fl:
+        if fl > 0:
             print(f"{us:9.1f} us {fl / us / 1e6:8.1f} TF/s  {key[1]}")
+        elif fl < 0:
+            print(f"{us:9.1f} us {-fl / us / 1e3:8.1f} GB/s   {key[1]}")
     print("---- per entry point (us/step, min over reps) ----")
     for n, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"{v:10.1f}  {n}")
