@@ -34,7 +34,8 @@ for step in ${STEPS:-tests smoke bench}; do
     cat $O/bench_c2.json ;;
   trace)   # kernel-trace stats of the bench command
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-fp32-line --no-graph-line > $O/trace.log 2>&1 || fail trace $O/trace.log
-    python tools/profsum.py $O/trace > $O/trace_summary.txt 2>&1; head -40 $O/trace_summary.txt ;;
+    # 78 traced steps: 5 warm-up + 30 timed + 10 probe + 2 hbm-probe + 31 fwd+bwd-only (without_optimizer)
+    python tools/profsum.py $O/trace 78 40 > $O/trace_summary.txt 2>&1; head -45 $O/trace_summary.txt ;;
   layerprof)
     timeout -k 10 300 python -u tools/layerprof.py > $O/layerprof.txt 2>&1 || fail layerprof $O/layerprof.txt
     tail -5 $O/layerprof.txt ;;
@@ -45,7 +46,17 @@ for step in ${STEPS:-tests smoke bench}; do
       timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $O/pmc$i -o pmc -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-fp32-line --no-graph-line > $O/pmc$i.log 2>&1 || fail "pmc pass $i" $O/pmc$i.log 5
     done
     python tools/traffic.py --all $O/pmc1 $O/pmc2 > $O/traffic.log 2>&1 || fail traffic $O/traffic.log
+    cp profiles/traffic.json $O/traffic.json
     tail -40 $O/traffic.log ;;
+  pmc5)    # the same two passes over the C5 workload (fp16 3x1024^2, one micro-step per step): traffic.json "@1024x3" keys
+    i=0
+    for set in FETCH_SIZE WRITE_SIZE; do
+      i=$((i+1))
+      timeout -s KILL 180 rocprofv3 --pmc $set --output-format csv -d $O/pmc5_$i -o pmc -- python bench.py --precision fp16 --in-ch 3 --size 1024 --steps 1 --warmup 1 --no-cpu-baseline --no-fp32-line --no-graph-line > $O/pmc5_$i.log 2>&1 || fail "pmc5 pass $i" $O/pmc5_$i.log 5
+    done
+    python tools/traffic.py --all $O/pmc5_1 $O/pmc5_2 @1024x3 > $O/traffic5.log 2>&1 || fail traffic5 $O/traffic5.log
+    cp profiles/traffic.json $O/traffic.json
+    grep "@1024x3" $O/traffic5.log | head -20 ;;
   sq)      # instruction mix of the conv5 / wgrad5 kernels (SQ counters, one pass)
     timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_BRANCH --kernel-include-regex "${SQRE:-conv5_kernel|wgrad5_kernel}" --output-format csv -d $O/sq -o sq -- python tools/layerprof.py > $O/sq.log 2>&1 || fail sq $O/sq.log 5
     python tools/pmcsum.py $O/sq "${SQRE:-conv5_kernel|wgrad5_kernel}" > $O/sq_summary.txt 2>&1; cat $O/sq_summary.txt | head -40 ;;

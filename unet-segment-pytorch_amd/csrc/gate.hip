@@ -19,13 +19,16 @@ static inline int rows_for(long long P, int C) {
   const int cl = chan_lanes_g(C);
   const int cblocks = (C + cl - 1) / cl;
   long long r = (2048 + cblocks - 1) / cblocks;
-  const long long maxr = (P + 63) / 64;
+  const long long maxr = (P + 15) / 16;   // >= 16 pixels per block (the 64^2 maps: 1024 blocks, not 256)
   if (r > maxr) r = maxr;
   if (r < 1) r = 1;
   return (int)r;
 }
+// blocks (= partial rows) of the per-pixel passes: >= 32 pixels per block, so the small maps (64^2: 16 K
+// pixels) still spread over 512 blocks — with 256 pixels per block that map ran on 64 blocks, a quarter
+// of the CUs (gate pass 1 at 64^2: 62 us for 84 MB, round-4 layerprof)
 static inline int pix_rows(long long P) {
-  long long r = (P + 255) / 256;
+  long long r = (P + 31) / 32;
   if (r > 2048) r = 2048;
   if (r < 1) r = 1;
   return (int)r;

@@ -691,9 +691,15 @@ __global__ __launch_bounds__(256) void convt_bwd_prep_kernel(long long N, int h,
   }
 }
 
-static inline int grid_for(long long total) {
+// block cap of a grid-stride launch (env override: A/B of the per-thread item count)
+static inline long long block_cap(const char* env, long long dflt) {
+  const char* e = getenv(env);
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? v : dflt;
+}
+static inline int grid_for(long long total, long long cap = 8192) {
   long long b = (total + 255) / 256;
-  if (b > 8192) b = 8192;
+  if (b > cap) b = cap;
   if (b < 1) b = 1;
   return (int)b;
 }
@@ -809,15 +815,15 @@ int unet_upsample_bwd(long long N, int C, int Hs, int Ws, int up_h, int up_w, in
   auto span = [](float sc, int up) { return sc > 0.f ? (int)floorf(2.f / sc) + 3 : up + 8; };
   if (C % 4 == 0 && span(sh, up_h) <= 8 && span(sw, up_w) <= 8) {
     if (total / 4 < (1LL << 31))
-      hipLaunchKernelGGL(upsample_bwd4w_kernel<unsigned>, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream,
+      hipLaunchKernelGGL(upsample_bwd4w_kernel<unsigned>, dim3(grid_for(total / 4, block_cap("UNET_UPB_BLOCKS", 8192))), dim3(256), 0, (hipStream_t)stream,
                          N, C, Hs, Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
     else
-      hipLaunchKernelGGL(upsample_bwd4w_kernel<unsigned long long>, dim3(grid_for(total / 4)), dim3(256), 0,
+      hipLaunchKernelGGL(upsample_bwd4w_kernel<unsigned long long>, dim3(grid_for(total / 4, block_cap("UNET_UPB_BLOCKS", 8192))), dim3(256), 0,
                          (hipStream_t)stream, N, C, Hs, Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
     return check_launch("upsample_bwd");
   }
   if (C % 4 == 0) {
-    hipLaunchKernelGGL(upsample_bwd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream, N, C, Hs,
+    hipLaunchKernelGGL(upsample_bwd4_kernel, dim3(grid_for(total / 4, block_cap("UNET_UPB_BLOCKS", 8192))), dim3(256), 0, (hipStream_t)stream, N, C, Hs,
                        Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
     return check_launch("upsample_bwd");
   }
@@ -1033,7 +1039,8 @@ int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, 
   const int vec = dtype != UNET_F32 ? 8 : 4;
   const long long total = N * H * (long long)W * ((src->C + vec - 1) / vec);
   long long b = (total + 255) / 256;
-  if (b > 16384) b = 16384;
+  const long long bcap = block_cap("UNET_MAT_BLOCKS", 4096);
+  if (b > bcap) b = bcap;
   const int cv = src->C / vec;
   // 32-bit gather offsets in item_issue: the source must stay below 4 GiB
   const double bytes = (double)N * src->H * src->W * src->C * (dtype != UNET_F32 ? 2 : 4);
