@@ -19,6 +19,9 @@
 
 namespace unet {
 
+#ifndef PW_PREFETCH
+#define PW_PREFETCH 0   // 1: the next wave tile's first loads issued before this tile's epilogue (more VGPRs)
+#endif
 constexpr unsigned PW_OOB = 0x40000000u;  // >= every tensor byte size admitted below (< 1 GiB)
 typedef __amdgpu_buffer_rsrc_t pw_rsrc_t;
 
@@ -58,7 +61,6 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
   typedef typename Mma<T>::frag F;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i16 = lane & 15, g = lane >> 4;
-  const long long pw0 = ((long long)blockIdx.x * 4 + wave) * (16 * NB);
   const int co0 = blockIdx.y * (16 * NA);
   const unet_src& s = d.src[0];
   const bool act = s.kind == UNET_SRC_ACT;
@@ -67,145 +69,203 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
   const pw_rsrc_t xr = pw_rsrc(s.data, (unsigned)(P * pixb));
   // packed weights [ntile][chunk][64 lanes][16 B] (1x1: one tap)
   const pw_rsrc_t wr = pw_rsrc(d.weight, (unsigned)((d.Cout + 127) / 128 * 8) * (unsigned)nchunks * 1024u);
+  // persistent over pixel tiles (16 NB pixels per wave tile, wave tiles grid-strided so that the waves in
+  // flight read neighbouring pixels): the set-up, the BN-sum reduction and the partial-row store are paid once
+  // per wave instead of once per tile, and the next tile's first loads are issued before this tile's epilogue
+  const long long ntiles = (P + 16 * NB - 1) / (16 * NB);
+  const long long tstride = (long long)gridDim.x * 4;
+  long long tile = (long long)blockIdx.x * 4 + wave;
 
   // this lane's pixels (one per px tile) and their gate multipliers; pixels past P read as 0 (OOB) and
   // are forced to 0 after the transform
   unsigned xoff[NB];
   float gm[NB];
+  uint4 xq[NB];
+  auto setup = [&](long long t) {
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const long long p = pw0 + 16 * b + i16;
-    const bool ok = p < P;
-    xoff[b] = ok ? (unsigned)p * pixb + (unsigned)g * 16u : PW_OOB;
-    gm[b] = ok ? 1.f : 0.f;
-    if (ok && act && s.gate_p) gm[b] = sigmoidf_(s.gate_p[p] * s.gate_ab[0] + s.gate_ab[1]);
-  }
+    for (int b = 0; b < NB; ++b) {
+      const long long p = t * (16 * NB) + 16 * b + i16;
+      const bool ok = t < ntiles && p < P;
+      xoff[b] = ok ? (unsigned)p * pixb + (unsigned)g * 16u : PW_OOB;
+      gm[b] = ok ? 1.f : 0.f;
+      if (ok && act && s.gate_p) gm[b] = sigmoidf_(s.gate_p[p] * s.gate_ab[0] + s.gate_ab[1]);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) xq[b] = pw_ld(xr, xoff[b], 0);
+  };
+#if PW_PREFETCH
+  setup(tile);
+#endif
 
-  f32x4 acc[NA][NB];
+  float sm[NA][4], sq[NA][4];   // OMK 0: BN partial sums over all of this wave's tiles (pixels past P add 0)
 #pragma unroll
   for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < NB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) { sm[a][r] = 0.f; sq[a][r] = 0.f; }
 
-  uint4 xq[NB];
+  for (; tile < ntiles; tile += tstride) {
+    const long long pw0 = tile * (16 * NB);
+#if !PW_PREFETCH
+    setup(tile);
+#endif
+    f32x4 acc[NA][NB];
 #pragma unroll
-  for (int b = 0; b < NB; ++b) xq[b] = pw_ld(xr, xoff[b], 0);
-  // fp32 gradient epilogue that accumulates: the old values are loaded here, ahead of the MFMAs (the
-  // compiler cannot hoist them over the stores, which it must assume alias; loaded in the epilogue, each
-  // read-modify-write was a full memory round trip per 16-byte column)
-  float4 old[NB][NA];
-  const bool rmw = OMK == 1 && (d.accum || d.accum2);
-  float4 gxs[GATED ? NB : 1][GATED ? NA : 1];
-  float gsv[GATED ? NB : 1];
-  if constexpr (GATED) {
-    const float* dxs = (const float*)d.pool_src.data;
-    const float ga = d.pool_src.gate_ab[0], gb = d.pool_src.gate_ab[1];
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const long long p = pw0 + 16 * b + i16;
-      gsv[b] = p < P ? sigmoidf_(d.pool_src.gate_p[p] * ga + gb) : 0.f;
+      for (int b = 0; b < NB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fp32 gradient epilogue that accumulates: the old values are loaded here, ahead of the MFMAs (the
+    // compiler cannot hoist them over the stores, which it must assume alias; loaded in the epilogue, each
+    // read-modify-write was a full memory round trip per 16-byte column)
+    float4 old[NB][NA];
+    const bool rmw = OMK == 1 && (d.accum || d.accum2);
+    float4 gxs[GATED ? NB : 1][GATED ? NA : 1];
+    float gsv[GATED ? NB : 1];
+    if constexpr (GATED) {
+      const float* dxs = (const float*)d.pool_src.data;
+      const float ga = d.pool_src.gate_ab[0], gb = d.pool_src.gate_ab[1];
 #pragma unroll
-      for (int a = 0; a < NA; ++a)
-        gxs[b][a] = p < P ? *reinterpret_cast<const float4*>(dxs + p * d.Cout + co0 + 16 * a + 4 * g)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-  if (rmw) {
-    const int c2 = d.Cout - d.split;
+      for (int b = 0; b < NB; ++b) {
+        const long long p = pw0 + 16 * b + i16;
+        gsv[b] = p < P ? sigmoidf_(d.pool_src.gate_p[p] * ga + gb) : 0.f;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const long long p = pw0 + 16 * b + i16;
-#pragma unroll
-      for (int a = 0; a < NA; ++a) {
-        const int co = co0 + 16 * a + 4 * g;
-        const bool first = co < d.split;
-        const int acc_in = first ? d.accum : d.accum2;
-        old[b][a] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p < P && acc_in)
-          old[b][a] = first ? *reinterpret_cast<const float4*>((const float*)d.out + p * d.split + co)
-                            : *reinterpret_cast<const float4*>((const float*)d.out2 + p * c2 + (co - d.split));
+        for (int a = 0; a < NA; ++a)
+          gxs[b][a] = p < P ? *reinterpret_cast<const float4*>(dxs + p * d.Cout + co0 + 16 * a + 4 * g)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-  }
-  for (int c = 0; c < nchunks; ++c) {
-    uint4 xn[NB];
-    if (c + 1 < nchunks) {
+    if (rmw) {
+      const int c2 = d.Cout - d.split;
 #pragma unroll
-      for (int b = 0; b < NB; ++b) xn[b] = pw_ld(xr, xoff[b], (unsigned)(c + 1) * 64u);
-    }
-    uint4 wq[NA];
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-      wq[a] = pw_ld(wr, (unsigned)lane * 16u, ((unsigned)(co0 / 16 + a) * nchunks + c) * 1024u);
-    float sc[8], sf[8];
-    if (act) {
-      const int ch = c * 32 + g * 8;
-      const float4 s0 = *reinterpret_cast<const float4*>(s.scale + ch);
-      const float4 s1 = *reinterpret_cast<const float4*>(s.scale + ch + 4);
-      const float4 f0 = *reinterpret_cast<const float4*>(s.shift + ch);
-      const float4 f1 = *reinterpret_cast<const float4*>(s.shift + ch + 4);
-      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-      sf[0] = f0.x; sf[1] = f0.y; sf[2] = f0.z; sf[3] = f0.w; sf[4] = f1.x; sf[5] = f1.y; sf[6] = f1.z; sf[7] = f1.w;
-    }
-    F xb[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) xb[b] = pw_act<T>(xq[b], act, sc, sf, lo, gm[b]);
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      const F wa = __builtin_bit_cast(F, wq[a]);
-#pragma unroll
-      for (int b = 0; b < NB; ++b) acc[a][b] = Mma<T>::mma(wa, xb[b], acc[a][b]);
-    }
-    if (c + 1 < nchunks) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b) xq[b] = xn[b];
-    }
-  }
-
-  // epilogue: acc[a][b][r] = out[px = pw0 + 16b + i16][co = co0 + 16a + 4g + r]
-  if constexpr (OMK == 0) {
-    T* y = (T*)d.out;
-    float sm[NA][4], sq[NA][4];
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { sm[a][r] = 0.f; sq[a][r] = 0.f; }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const long long p = pw0 + 16 * b + i16;
-      if constexpr (NA % 2 == 0) {
-        // lane (i16, g) holds channels 16 a + 4 g .. + 3 of pixel p: v_permlane16_swap of the packed (a, a + 1)
-        // pairs leaves row g with the 8 contiguous channels 16 (a + (g & 1)) + 8 (g >> 1) .. + 7, stored as one
-        // 16-byte vector (smallcin.hip's epilogue); every lane takes part in the swaps, the stores are masked
-#pragma unroll
-        for (int a = 0; a < NA; a += 2) {
-          const f32x4 v0 = acc[a][b], v1 = acc[a + 1][b];
-          const auto sx = __builtin_amdgcn_permlane16_swap(pack2_16<T>(v0[0], v0[1]), pack2_16<T>(v1[0], v1[1]),
-                                                           false, false);
-          const auto sy = __builtin_amdgcn_permlane16_swap(pack2_16<T>(v0[2], v0[3]), pack2_16<T>(v1[2], v1[3]),
-                                                           false, false);
-          if (p < P)
-            *reinterpret_cast<uint4*>(y + p * d.Cout + co0 + 16 * (a + (g & 1)) + 8 * (g >> 1)) =
-                make_uint4(sx[0], sy[0], sx[1], sy[1]);
-        }
-      } else {
+      for (int b = 0; b < NB; ++b) {
+        const long long p = pw0 + 16 * b + i16;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
           const int co = co0 + 16 * a + 4 * g;
-          if (p < P) {
-            const f32x4 v = acc[a][b];
-            *reinterpret_cast<uint2*>(y + p * d.Cout + co) = make_uint2(pack2_16<T>(v[0], v[1]), pack2_16<T>(v[2], v[3]));
-          }
+          const bool first = co < d.split;
+          const int acc_in = first ? d.accum : d.accum2;
+          old[b][a] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (p < P && acc_in)
+            old[b][a] = first ? *reinterpret_cast<const float4*>((const float*)d.out + p * d.split + co)
+                              : *reinterpret_cast<const float4*>((const float*)d.out2 + p * c2 + (co - d.split));
         }
       }
+    }
+    for (int c = 0; c < nchunks; ++c) {
+      uint4 xn[NB];
+      if (c + 1 < nchunks) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) xn[b] = pw_ld(xr, xoff[b], (unsigned)(c + 1) * 64u);
+      }
+      uint4 wq[NA];
 #pragma unroll
       for (int a = 0; a < NA; ++a)
+        wq[a] = pw_ld(wr, (unsigned)lane * 16u, ((unsigned)(co0 / 16 + a) * nchunks + c) * 1024u);
+      float sc[8], sf[8];
+      if (act) {
+        const int ch = c * 32 + g * 8;
+        const float4 s0 = *reinterpret_cast<const float4*>(s.scale + ch);
+        const float4 s1 = *reinterpret_cast<const float4*>(s.scale + ch + 4);
+        const float4 f0 = *reinterpret_cast<const float4*>(s.shift + ch);
+        const float4 f1 = *reinterpret_cast<const float4*>(s.shift + ch + 4);
+        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+        sf[0] = f0.x; sf[1] = f0.y; sf[2] = f0.z; sf[3] = f0.w; sf[4] = f1.x; sf[5] = f1.y; sf[6] = f1.z; sf[7] = f1.w;
+      }
+      F xb[NB];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {  // pixels past P accumulated exact zeros
-          sm[a][r] += acc[a][b][r];
-          sq[a][r] += acc[a][b][r] * acc[a][b][r];
-        }
+      for (int b = 0; b < NB; ++b) xb[b] = pw_act<T>(xq[b], act, sc, sf, lo, gm[b]);
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const F wa = __builtin_bit_cast(F, wq[a]);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] = Mma<T>::mma(wa, xb[b], acc[a][b]);
+      }
+      if (c + 1 < nchunks) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) xq[b] = xn[b];
+      }
     }
+#if PW_PREFETCH
+    // the next tile's pixels and first chunk, in flight during this tile's epilogue
+    setup(tile + tstride);
+#endif
+
+    // epilogue: acc[a][b][r] = out[px = pw0 + 16b + i16][co = co0 + 16a + 4g + r]
+    if constexpr (OMK == 0) {
+      T* y = (T*)d.out;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const long long p = pw0 + 16 * b + i16;
+        if constexpr (NA % 2 == 0) {
+          // lane (i16, g) holds channels 16 a + 4 g .. + 3 of pixel p: v_permlane16_swap of the packed (a, a + 1)
+          // pairs leaves row g with the 8 contiguous channels 16 (a + (g & 1)) + 8 (g >> 1) .. + 7, stored as one
+          // 16-byte vector (smallcin.hip's epilogue); every lane takes part in the swaps, the stores are masked
+#pragma unroll
+          for (int a = 0; a < NA; a += 2) {
+            const f32x4 v0 = acc[a][b], v1 = acc[a + 1][b];
+            const auto sx = __builtin_amdgcn_permlane16_swap(pack2_16<T>(v0[0], v0[1]), pack2_16<T>(v1[0], v1[1]),
+                                                             false, false);
+            const auto sy = __builtin_amdgcn_permlane16_swap(pack2_16<T>(v0[2], v0[3]), pack2_16<T>(v1[2], v1[3]),
+                                                             false, false);
+            if (p < P)
+              *reinterpret_cast<uint4*>(y + p * d.Cout + co0 + 16 * (a + (g & 1)) + 8 * (g >> 1)) =
+                  make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          }
+        } else {
+#pragma unroll
+          for (int a = 0; a < NA; ++a) {
+            const int co = co0 + 16 * a + 4 * g;
+            if (p < P) {
+              const f32x4 v = acc[a][b];
+              *reinterpret_cast<uint2*>(y + p * d.Cout + co) = make_uint2(pack2_16<T>(v[0], v[1]), pack2_16<T>(v[2], v[3]));
+            }
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // pixels past P accumulated exact zeros
+            sm[a][r] += acc[a][b][r];
+            sq[a][r] += acc[a][b][r] * acc[a][b][r];
+          }
+      }
+    } else {  // UNET_OUT_F32 (host-checked: split % 4 == 0)
+      float* o1 = (float*)d.out;
+      float* o2 = (float*)d.out2;
+      const int c2 = d.Cout - d.split;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const long long p = pw0 + 16 * b + i16;
+        if (p >= P) continue;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          const int co = co0 + 16 * a + 4 * g;
+          float4* q = co < d.split ? reinterpret_cast<float4*>(o1 + p * d.split + co)
+                                   : reinterpret_cast<float4*>(o2 + p * c2 + (co - d.split));
+          float4 v = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
+          if constexpr (GATED) {
+            // the x*s term as gate_bwd1 formed it (old + d*s, or d*s), then + W_x^T dy as the separate
+            // accumulating dgrad added it: the same fp32 operations in the same order
+            const float4 x = gxs[b][a];
+            const float sg = gsv[b];
+            float4 t;
+            if (d.accum) {
+              const float4 o = *q;
+              t = make_float4(__builtin_fmaf(x.x, sg, o.x), __builtin_fmaf(x.y, sg, o.y), __builtin_fmaf(x.z, sg, o.z),
+                              __builtin_fmaf(x.w, sg, o.w));
+            } else {
+              t = make_float4(x.x * sg, x.y * sg, x.z * sg, x.w * sg);
+            }
+            v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+          } else if (rmw && (co < d.split ? d.accum : d.accum2)) {
+            const float4 o = old[b][a];
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *q = v;
+        }
+      }
+    }
+  }
+  if constexpr (OMK == 0) {
     if (d.stats) {
       __shared__ float red[4][NA * 16][2];
 #pragma unroll
@@ -224,41 +284,6 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
         const float w = red[0][tid][1] + red[1][tid][1] + red[2][tid][1] + red[3][tid][1];
         d.stats[(size_t)co * gridDim.x + blockIdx.x] = u;
         d.stats[((size_t)d.Cout + co) * gridDim.x + blockIdx.x] = w;
-      }
-    }
-  } else {  // UNET_OUT_F32 (host-checked: split % 4 == 0)
-    float* o1 = (float*)d.out;
-    float* o2 = (float*)d.out2;
-    const int c2 = d.Cout - d.split;
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const long long p = pw0 + 16 * b + i16;
-      if (p >= P) continue;
-#pragma unroll
-      for (int a = 0; a < NA; ++a) {
-        const int co = co0 + 16 * a + 4 * g;
-        float4* q = co < d.split ? reinterpret_cast<float4*>(o1 + p * d.split + co)
-                                 : reinterpret_cast<float4*>(o2 + p * c2 + (co - d.split));
-        float4 v = make_float4(acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]);
-        if constexpr (GATED) {
-          // the x*s term as gate_bwd1 formed it (old + d*s, or d*s), then + W_x^T dy as the separate
-          // accumulating dgrad added it: the same fp32 operations in the same order
-          const float4 x = gxs[b][a];
-          const float sg = gsv[b];
-          float4 t;
-          if (d.accum) {
-            const float4 o = *q;
-            t = make_float4(__builtin_fmaf(x.x, sg, o.x), __builtin_fmaf(x.y, sg, o.y), __builtin_fmaf(x.z, sg, o.z),
-                            __builtin_fmaf(x.w, sg, o.w));
-          } else {
-            t = make_float4(x.x * sg, x.y * sg, x.z * sg, x.w * sg);
-          }
-          v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
-        } else if (rmw && (co < d.split ? d.accum : d.accum2)) {
-          const float4 o = old[b][a];
-          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
-        }
-        *q = v;
       }
     }
   }
@@ -527,16 +552,30 @@ static void pw_conv_geom(const unet_conv_desc* d, int& na, int& nb) {
   nb = 4;
 }
 
+// blocks along the pixels: the pw_conv_kernel waves are persistent over wave tiles (16 NB pixels each); up to
+// PW_BLOCKS blocks of 4 waves, i.e. 8 tiles per wave on the 512^2 maps (UNET_PW_BLOCKS: A/B override).  Round-4
+// layer sweep (tools/gpu_r04.sh lp): one tile per wave 797 us/step for the 1x1 fwd + dgrads, 1024 blocks 758,
+// 512 blocks 739 (profiles/r04_pw_persistent_sweep.txt)
+constexpr long long PW_BLOCKS = 512;
+static int pw_blocks(const unet_conv_desc* d, int nb) {
+  const long long P = (long long)d->N * d->H * d->W;
+  const long long tiles = cdiv(P, 16 * nb);
+  const char* e = getenv("UNET_PW_BLOCKS");
+  const long long cap = e && atoll(e) > 0 ? atoll(e) : PW_BLOCKS;
+  long long b = cdiv(tiles, 4);
+  return (int)(b < cap ? b : cap);
+}
+
 int pw_conv_rows(const unet_conv_desc* d) {
   int na, nb;
   pw_conv_geom(d, na, nb);
-  return cdiv((long long)d->N * d->H * d->W, 64 * nb);
+  return pw_blocks(d, nb);
 }
 
 template <typename T, int NA, int NB>
 static int launch_pw(const unet_conv_desc* d, hipStream_t st) {
   const long long P = (long long)d->N * d->H * d->W;
-  dim3 grid(cdiv(P, 64 * NB), d->Cout / (16 * NA));
+  dim3 grid(pw_blocks(d, NB), d->Cout / (16 * NA));
   if (d->out_mode == UNET_OUT_F32_GATED)
     hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 2>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
   else if (d->out_mode == UNET_OUT_F32)
