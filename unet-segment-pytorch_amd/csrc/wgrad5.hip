@@ -445,7 +445,9 @@ static W5Plan wgrad5_plan(const unet_wgrad_desc* d) {
   // one resident block per CU: at least 256 blocks, the split count a multiple of 8 (the blocks of one
   // split — same pixels, other channel blocks — then share an XCD and its L2); slabs capped at 160 MB
   long long s = (256 + tiles_out - 1) / tiles_out;
-  s = (s + 7) / 8 * 8;
+  // (a layer whose channel tiles alone fill >= 32 of the CUs keeps its few splits: rounding 4 up to 8 doubled
+  // the slab traffic of the 1024 -> 512 weight gradient at 64^2, 151 instead of 75 MB; UNET_W5_SPLIT8=1: old rule)
+  if (s > 8 || getenv("UNET_W5_SPLIT8")) s = (s + 7) / 8 * 8;
   const long long cap = (long long)(((size_t)160 << 20) / slab);
   if (s > cap) s = cap;
   if (s > p.mtiles) s = p.mtiles;
