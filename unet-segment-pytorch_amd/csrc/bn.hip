@@ -115,7 +115,9 @@ static inline int chan_lanes(int C) {
 static inline int reduce_rows(long long P, int C) {
   const int cl = chan_lanes(C);
   const int cblocks = (C + cl - 1) / cl;
-  long long r = (2048 + cblocks - 1) / cblocks;
+  const char* e = getenv("UNET_BN_ROWS");   // A/B of the partial-row count (default 2048 blocks)
+  const long long want = e && atoll(e) > 0 ? atoll(e) : 2048;
+  long long r = (want + cblocks - 1) / cblocks;
   const long long maxr = (P + 63) / 64;  // at least 64 pixels per block
   if (r > maxr) r = maxr;
   if (r < 1) r = 1;
@@ -374,7 +376,9 @@ static inline bool bn_vec_ok(int C) {
 static inline int reduce_rows_vec(long long P, int C) {
   const int R = 256 / (C / 8);
   long long r = (P + 8LL * R - 1) / (8LL * R);  // >= 8 pixel iterations per thread
-  if (r > 2048) r = 2048;
+  const char* e = getenv("UNET_BN_ROWS");        // A/B of the partial-row cap (default 2048 blocks)
+  const long long cap = e && atoll(e) > 0 ? atoll(e) : 2048;
+  if (r > cap) r = cap;
   if (r < 1) r = 1;
   return (int)r;
 }
