@@ -450,10 +450,6 @@ static W5Plan wgrad5_plan(const unet_wgrad_desc* d) {
   if (s > 8 || getenv("UNET_W5_SPLIT8")) s = (s + 7) / 8 * 8;
   const long long cap = (long long)(((size_t)160 << 20) / slab);
   if (s > cap) s = cap;
-  if (const char* e = getenv("UNET_W5_MAXSPLIT")) {   // A/B: fewer slabs (less slab traffic) vs parallelism
-    const long long m = atoll(e);
-    if (m > 0 && s > m) s = m;
-  }
   if (s > p.mtiles) s = p.mtiles;
   if (s < 1) s = 1;
   p.per_split = cdiv(p.mtiles, (int)s);
