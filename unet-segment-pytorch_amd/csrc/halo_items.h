@@ -13,6 +13,10 @@
 #pragma once
 #include "conv_common.h"
 
+#ifndef UNET_PK_UP
+#define UNET_PK_UP 0   // 1: the bilinear source transform on packed fp32 (A/B build)
+#endif
+
 namespace unet {
 
 template <typename T>
@@ -148,6 +152,29 @@ __device__ __forceinline__ void item_finish(const D& d, const SrcView& s, const 
       unpack16<T>(it.q[1], t1);
       unpack16<T>(it.q[2], t2);
       unpack16<T>(it.q[3], t3);
+#if UNET_PK_UP
+      // channel pairs on packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: half the VALU of the BN apply and the blend;
+      // ReLU stays per element, gfx950 has no packed fp32 max)
+      typedef __attribute__((ext_vector_type(2))) float f2;
+      const f2 w0 = {it.w0, it.w0}, w1 = {it.w1, it.w1}, w2 = {it.w2, it.w2}, w3 = {it.w3, it.w3};
+#pragma unroll
+      for (int j = 0; j < VEC; j += 2) {
+        const f2 c = {sc[j], sc[j + 1]}, f = {sf[j], sf[j + 1]};
+        f2 a0 = __builtin_elementwise_fma(f2{t0[j], t0[j + 1]}, c, f);
+        f2 a1 = __builtin_elementwise_fma(f2{t1[j], t1[j + 1]}, c, f);
+        f2 a2 = __builtin_elementwise_fma(f2{t2[j], t2[j + 1]}, c, f);
+        f2 a3 = __builtin_elementwise_fma(f2{t3[j], t3[j + 1]}, c, f);
+        if (s.relu) {
+          a0 = f2{fmaxf(a0[0], 0.f), fmaxf(a0[1], 0.f)};
+          a1 = f2{fmaxf(a1[0], 0.f), fmaxf(a1[1], 0.f)};
+          a2 = f2{fmaxf(a2[0], 0.f), fmaxf(a2[1], 0.f)};
+          a3 = f2{fmaxf(a3[0], 0.f), fmaxf(a3[1], 0.f)};
+        }
+        const f2 r = __builtin_elementwise_fma(w3, a3, __builtin_elementwise_fma(w2, a2, __builtin_elementwise_fma(w1, a1, w0 * a0)));
+        v[j] = r[0];
+        v[j + 1] = r[1];
+      }
+#else
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         float a0 = t0[j] * sc[j] + sf[j], a1 = t1[j] * sc[j] + sf[j];
@@ -155,6 +182,7 @@ __device__ __forceinline__ void item_finish(const D& d, const SrcView& s, const 
         if (s.relu) { a0 = fmaxf(a0, 0.f); a1 = fmaxf(a1, 0.f); a2 = fmaxf(a2, 0.f); a3 = fmaxf(a3, 0.f); }
         v[j] = it.w0 * a0 + it.w1 * a1 + it.w2 * a2 + it.w3 * a3;
       }
+#endif
     }
   } else {
 #pragma unroll
