@@ -14,7 +14,8 @@
 #include "conv_common.h"
 
 #ifndef UNET_PK_UP
-#define UNET_PK_UP 0   // 1: the bilinear source transform on packed fp32 (A/B build)
+#define UNET_PK_UP 1   // the bilinear source transform on packed fp32 (0: the per-element form, for A/B builds;
+                       // round-4 A/B: materialise 169 -> 141 us/step)
 #endif
 
 namespace unet {

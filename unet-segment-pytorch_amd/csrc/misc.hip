@@ -92,7 +92,9 @@ __global__ __launch_bounds__(256) void upsample_bwd4w_kernel(long long N, int C,
       wy[k] = (u <= uhi && yy >= 0 && yy < Hp) ? up_weight(sh, u, Hs, i) : 0.f;
       wx[k] = (v <= vhi && xx >= 0 && xx < Wp) ? up_weight(sw, v, Ws, j) : 0.f;
     }
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    // the 4 channels as two packed fp32 pairs (v_pk_fma_f32): the same fused multiply-add per channel
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    f2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
 #pragma unroll
     for (int ky = 0; ky < 8; ++ky) {
       if (wy[ky] == 0.f) continue;
@@ -102,9 +104,16 @@ __global__ __launch_bounds__(256) void upsample_bwd4w_kernel(long long N, int C,
         if (wx[kx] == 0.f) continue;
         const float4 g = row[(long long)(vlo + kx + pl) * C4];
         const float w = wy[ky] * wx[kx];
-        acc.x += w * g.x; acc.y += w * g.y; acc.z += w * g.z; acc.w += w * g.w;
+#if UNET_PK_UP
+        const f2 ww = {w, w};
+        a01 = __builtin_elementwise_fma(ww, f2{g.x, g.y}, a01);
+        a23 = __builtin_elementwise_fma(ww, f2{g.z, g.w}, a23);
+#else
+        a01[0] += w * g.x; a01[1] += w * g.y; a23[0] += w * g.z; a23[1] += w * g.w;
+#endif
       }
     }
+    float4 acc = make_float4(a01[0], a01[1], a23[0], a23[1]);
     float4* o = reinterpret_cast<float4*>(dx) + e;
     if (accum) {
       const float4 a = *o;
