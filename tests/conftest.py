@@ -18,6 +18,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+# Run last: the long trajectory tests (200-epoch chaotic overfit protocol).  Under `-x`, a failure there must
+# not keep the deterministic golden-fixture parity tests from running.
+_LAST = ("test_gpu_overfit.py",)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=lambda it: any(it.nodeid.split("::")[0].endswith(f) for f in _LAST))
+
+
 def load_golden(name: str):
     import torch
     return torch.load(GOLDEN / name, weights_only=True)

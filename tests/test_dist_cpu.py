@@ -117,3 +117,19 @@ def test_bench_time_is_max_over_ranks():
 def test_single_process_time_passthrough():
     import bench
     assert bench.max_over_ranks(3.5, torch.device("cpu")) == 3.5
+
+
+def test_graphed_train_step_refuses_ddp():
+    """GraphedTrainStep takes its gradients on leaf aliases of the parameters, so a DDP-wrapped
+    model's reducer hooks would never fire; it must refuse DDP up front (before touching any device)."""
+    from unet.utils.graphed import GraphedTrainStep
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        ddp = torch.nn.parallel.DistributedDataParallel(torch.nn.Linear(4, 2))
+        opt = torch.optim.AdamW(ddp.parameters(), lr=1e-3, capturable=True)
+        with pytest.raises(RuntimeError, match="DDP"):
+            GraphedTrainStep(ddp, torch.nn.functional.mse_loss, opt, (2, 4), (2, 2))
+    finally:
+        dist.destroy_process_group()

@@ -253,10 +253,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int
   // 4 pixels per trip without the pooled gradient (17.6 -> 15.7 us per launch); with it the extra registers
   // cost more than the overlap gains (59 -> 64 us), so one.  The pooled gradient's pixel coordinates advance
   // by the fixed step R (pix_adv) instead of two 32-bit divisions per pixel
-#ifndef BNR_POOL_U
-#define BNR_POOL_U 1
-#endif
-  constexpr int BNR_U = POOL ? BNR_POOL_U : 4;
+  // (the pooled form must stay at one pixel per trip: its cursor pc only tracks p while p < p1)
+  constexpr int BNR_U = POOL ? 1 : 4;
   PixCur pc{0, 0, 0};
   const unsigned sq = POOL ? (unsigned)R / (unsigned)(pg.W > 0 ? pg.W : 1) : 0u, sr = POOL ? (unsigned)R - sq * (unsigned)pg.W : 0u;
   if (POOL && py < R && p0 + py < p1) pc = pix_cur(pg, (unsigned)(p0 + py));

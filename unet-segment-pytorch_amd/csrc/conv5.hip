@@ -40,6 +40,7 @@ constexpr int C5_WM = 4;                 // wave row groups of a workgroup tile
 constexpr int C5_WH = 2;                 // 32-channel halves of the block's 64 output channels
 constexpr int C5_BN = 64;                // output channels per workgroup
 constexpr int C5_CMAX = 1024;            // largest BN-activation source (scale / shift table)
+constexpr int C5_TABS = C5_CMAX + 8;     // table stride: each half carries its own 8-float zero pad
 constexpr int C5_NPAD = PACK_NPAD;       // packed weight rows are padded to this (conv_common.h)
 constexpr int OM5_Y = 0, OM5_F32 = 1, OM5_BNB = 2;
 
@@ -60,7 +61,7 @@ struct C5Layout {
   static constexpr int OFF_GATE = OFF_W + 3 * WIMG;
   static constexpr int GATE = NI * 256;             // per-lane gate pre-activations of one tile
   static constexpr int OFF_TAB = OFF_GATE + (ACT ? 2 * GATE : 0);
-  static constexpr int OFF_BTAB = OFF_TAB + (ACT ? 2 * C5_CMAX * 4 : 0);   // BNB: the block's BN affine
+  static constexpr int OFF_BTAB = OFF_TAB + (ACT ? 2 * C5_TABS * 4 : 0);   // BNB: the block's BN affine
   static constexpr int OFF_JUNK = OFF_BTAB + 2 * C5_BN * 4;                   // target of the filler DMAs
   static constexpr int BYTES = OFF_JUNK + 1024;
 };
@@ -287,8 +288,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
         const bool ok = xok[k] && !(rag && hbit[k]);
         const float4 a0 = *reinterpret_cast<const float4*>(tab + ch);
         const float4 a1 = *reinterpret_cast<const float4*>(tab + ch + 4);
-        const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_CMAX + ch);
-        const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_CMAX + ch + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_TABS + ch);
+        const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_TABS + ch + 4);
         const f2_t sc[4] = {{a0.x, a0.y}, {a0.z, a0.w}, {a1.x, a1.y}, {a1.z, a1.w}};
         const f2_t sf[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
         float gm = ok ? 1.f : 0.f;
@@ -326,8 +327,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   // ---- prologue: scale/shift table, chunks 0-2 in flight, chunk 0 ready ----
   if constexpr (ACT) {
     float* tab = reinterpret_cast<float*>(lds + Lay::OFF_TAB);
-    for (int c = tid; c < C0; c += NT) { tab[c] = s0.scale[c]; tab[C5_CMAX + c] = s0.shift[c]; }
-    if (tid < 8) { tab[C0 + tid] = 0.f; tab[C5_CMAX + C0 + tid] = 0.f; }
+    for (int c = tid; c < C0; c += NT) { tab[c] = s0.scale[c]; tab[C5_TABS + c] = s0.shift[c]; }
+    if (tid < 8) { tab[C0 + tid] = 0.f; tab[C5_TABS + C0 + tid] = 0.f; }   // C0 <= C5_CMAX: inside each half
   }
   if constexpr (OM == OM5_BNB) {
     // the BN affine of the activation whose gradient this dgrad writes (its ReLU mask), the block's channels

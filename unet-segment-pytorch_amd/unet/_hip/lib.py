@@ -131,9 +131,67 @@ _SIGS = {
 
 _lib = None
 
+# UNET_GUARD=1: bounds-checking debug mode (csrc/guard_alloc.cpp).  Every device allocation of the process
+# gets guard bands and every library call is bracketed by a device sync + a check of all bands, so an
+# out-of-bounds write is named at the call that made it (or "before" it: a torch op in between).  Must be
+# set before the first CUDA allocation of the process; slow (no caching allocator); debug runs only.
+_GUARD = os.environ.get("UNET_GUARD", "") not in ("", "0")
+_guard = None
+# queries that launch nothing
+_NO_LAUNCH = {"unet_last_error", "unet_version", "unet_conv_mtiles", "unet_conv_stats_rows", "unet_conv_variant",
+              "unet_wgrad_variant", "unet_conv_act_out_ok", "unet_packed_weight_elems", "unet_wgrad_workspace",
+              "unet_bn_bwd_reduce_rows", "unet_gate_psi_rows", "unet_gate_bwd2_rows", "unet_convt_bwd_rows",
+              "unet_outconv_rows", "unet_loss_rows"}
+
 
 class HipLibraryError(RuntimeError):
     pass
+
+
+class GuardViolation(RuntimeError):
+    pass
+
+
+def _install_guard():
+    global _guard
+    if _guard is None:
+        path = _LIB_PATH.parent / "libunet_guard.so"
+        alloc = torch.cuda.memory.CUDAPluggableAllocator(str(path), "unet_guard_malloc", "unet_guard_free")
+        torch.cuda.memory.change_current_allocator(alloc)
+        g = ctypes.CDLL(str(path))
+        g.unet_guard_check.restype = c_int
+        g.unet_guard_check.argtypes = [ctypes.c_char_p, c_int]
+        g.unet_guard_allocations.restype = ctypes.c_long
+        _guard = g
+    return _guard
+
+
+def guard_check(where: str):
+    """UNET_GUARD mode: raise GuardViolation if any allocation's guard band was written."""
+    buf = ctypes.create_string_buffer(400)
+    if _guard is not None and _guard.unet_guard_check(buf, 400):
+        raise GuardViolation(f"{where}: {buf.value.decode()}")
+
+
+class _GuardedLib:
+    def __init__(self, lib):
+        self._lib = lib
+
+    def __getattr__(self, name):
+        fn = getattr(self._lib, name)
+        if name in _NO_LAUNCH:
+            return fn
+
+        def wrapped(*args):
+            guard_check(f"before {name} (a torch op since the previous library call)")
+            rc = fn(*args)
+            guard_check(name)
+            return rc
+        return wrapped
+
+
+if _GUARD:
+    _install_guard()
 
 
 def library_path() -> Path:
@@ -153,7 +211,7 @@ def load(require_gpu: bool = False):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        _lib = lib
+        _lib = _GuardedLib(lib) if _GUARD else lib
     if require_gpu and not torch.cuda.is_available():
         raise HipLibraryError("unet HIP path needs a ROCm GPU (MI355X / gfx950); none is visible.")
     return _lib

@@ -70,6 +70,10 @@ class GraphedTrainStep:
     def __init__(self, model: torch.nn.Module, criterion: Callable, optimizer: torch.optim.Optimizer,
                  input_shape: Sequence[int], target_shape: Sequence[int], target_dtype=torch.int64,
                  clip_norm: Optional[float] = 1.0, warmup: int = 3, device="cuda"):
+        if isinstance(model, torch.nn.parallel.DistributedDataParallel):
+            raise RuntimeError("GraphedTrainStep: the captured step takes gradients on leaf aliases of the "
+                               "parameters, so DDP's reducer hooks would never fire (each rank would train on "
+                               "its own unsynchronised gradients); graph the single-GPU step, or use eager DDP")
         if not isinstance(optimizer, (torch.optim.Adam, torch.optim.AdamW)):
             raise RuntimeError(f"GraphedTrainStep: needs torch.optim.Adam / AdamW (capturable=True), got "
                                f"{type(optimizer).__name__}: undoing the warm-up steps restores Adam's fresh state")
