@@ -14,7 +14,8 @@ from test_gpu_ops import DT, TN, _act_ref, _act_src, _close_bf16, _conv, _lib, _
 pytestmark = pytest.mark.gpu
 
 Y_SHAPES = [(4, 512, 512, 64, 64), (4, 256, 256, 64, 128), (4, 256, 256, 128, 128), (4, 128, 128, 256, 256),
-            (3, 200, 328, 64, 128), (8, 258, 98, 96, 64)]
+            (3, 200, 328, 64, 128), (8, 258, 98, 96, 64),
+            (2, 128, 128, 1024, 256)]   # a 1024-channel (C5_CMAX) activation: the scale / shift table's padding
 
 
 PATH = {"conv5": {"UNET_CONV5": "1"}}

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 GPU evidence, one parameterised script (replaces round 3's one-off gpu_r03*.sh files).
-#   TAG=<dir under gpurun_out>  STEPS="tests smoke bench c5 c2 trace layerprof pmc sq ablate ab lp gdiag repro"  bash tools/gpu_r04.sh
+# GPU evidence steps, one parameterised script.
+#   TAG=<dir under gpurun_out>  STEPS="tests smoke bench c5 c2 trace layerprof pmc sq ablate ab lp gdiag repro"  bash tools/gpu_steps.sh
 # Every GPU step runs under its own time limit; the chain stops at the first failure (no retries).
 set -o pipefail
-O=gpurun_out/${TAG:-r04}
+O=gpurun_out/${TAG:-run}
 mkdir -p $O
 export TMPDIR=/tmp
 fail() { echo "$1 failed"; tail -${3:-30} "$2"; exit 1; }
@@ -78,6 +78,9 @@ for step in ${STEPS:-tests smoke bench}; do
       env $v timeout -k 10 300 python -u tools/layerprof.py > "$f" 2>&1 || fail "lp $v" "$f"
       echo "[$v]"; grep -E "${LPGREP:-total}" "$f" | head -${LPN:-20}
     done ;;
+  guard)   # bounds-checked sweep (UNET_GUARD=1: guard bands around every allocation, checked after every library call)
+    UNET_GUARD=1 timeout -k 10 ${TLIM:-900} python -u tools/guard_sweep.py ${GUARDARGS} > $O/guard.log 2>&1 || fail guard $O/guard.log 40
+    grep -v amdgpu.ids $O/guard.log | tail -25 ;;
   gdiag)
     timeout -k 10 180 python -u tools/graphed_diag.py > $O/graphed_diag.log 2>&1 || fail gdiag $O/graphed_diag.log 40
     cat $O/graphed_diag.log | grep -v amdgpu.ids ;;

@@ -88,6 +88,14 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// XCD-aware block order (cdna_hip_programming.md T1): the hardware deals blocks b, b + 8, ... to one XCD; this
+// bijection on [0, nb) gives each XCD a contiguous range of logical blocks, so neighbouring logical blocks (which
+// share input rows) share one L2.  Speed only: correctness never depends on the placement.
+__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned nb) {
+  const unsigned q = nb >> 3, r = nb & 7u, x = b & 7u, k = b >> 3;
+  return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + k;
+}
+
 // ------------------------------------------------------------------------------------------------
 // error plumbing
 // ------------------------------------------------------------------------------------------------

@@ -123,6 +123,99 @@ __global__ __launch_bounds__(256) void upsample_bwd4w_kernel(long long N, int C,
   }
 }
 
+// Tiled adjoint (round 5): a block owns one source row i of image n, UJ source columns and 64 channels.
+//  phase 1 (vertical): t[v][c] = sum_u wy(u, i) d_up[u + pt][v + pl][c] for the tile's destination columns v, each
+//    d_up vector loaded once per block (the block-uniform row window and weights: no per-element index math, no
+//    divergent branches, ~11 independent 16-byte loads in flight per thread); t lands in LDS;
+//  phase 2 (horizontal): dx[i][j][c] (+)= sum_v wx(v, j) t[v][c] from LDS, the column weights from a per-block
+//    table of the window columns' (i0, lambda).
+//  Logical blocks run (channel tile, column tile, row, image) fastest-first and are dealt contiguously per XCD
+//    (xcd_block), so the d_up rows shared by source rows i and i + 1 are fetched into one XCD's L2 once; the
+//    element-per-thread gather measured 1.44x its algorithmic HBM bytes.
+//  Summation order: rows first, then columns (fixed: deterministic; fp32-rounding-level different from the
+//  per-element kernel's w_y * w_x products).
+constexpr int UPB_J = 16, UPB_CT = 16, UPB_VMAX = 56;
+__global__ __launch_bounds__(256) void upsample_bwd_tile_kernel(int N, int C, int Hs, int Ws, int up_h, int up_w, int pt,
+                                                                int pl, int Hp, int Wp, float sh, float sw,
+                                                                const float* __restrict__ dup, float* dx, int accum,
+                                                                int ntj, int ntc) {
+  __shared__ float4 t[UPB_VMAX][UPB_CT];
+  __shared__ int tab_i0[UPB_VMAX], tab_i1[UPB_VMAX];
+  __shared__ float tab_l[UPB_VMAX];
+  const int tid = threadIdx.x;
+  const unsigned lb = xcd_block(blockIdx.x, gridDim.x);
+  const int ct = (int)(lb % (unsigned)ntc);
+  unsigned r = lb / (unsigned)ntc;
+  const int jt = (int)(r % (unsigned)ntj);
+  r /= (unsigned)ntj;
+  const int i = (int)(r % (unsigned)Hs);
+  const int n = (int)(r / (unsigned)Hs);
+  const int C4 = C >> 2, c4 = ct * UPB_CT + (tid & (UPB_CT - 1));
+  const int j0 = jt * UPB_J;
+  // destination rows touching source row i (same window and +-1 guard as upsample_bwd4w; host-checked <= 8)
+  const int ulo = max(0, (int)ceilf((float)(i - 1) / sh) - 1), uhi = min(up_h - 1, (int)floorf((float)(i + 1) / sh) + 1);
+  float wy[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int u = ulo + k, yy = u + pt;
+    wy[k] = (u <= uhi && yy >= 0 && yy < Hp) ? up_weight(sh, u, Hs, i) : 0.f;
+  }
+  // destination columns touching source columns [j0, j0 + UPB_J) (host-checked <= UPB_VMAX)
+  const int jlast = min(Ws - 1, j0 + UPB_J - 1);
+  const int vlo = max(0, (int)ceilf((float)(j0 - 1) / sw) - 1), vhi = min(up_w - 1, (int)floorf((float)(jlast + 1) / sw) + 1);
+  const int nv = vhi - vlo + 1;
+  if (tid < nv) {
+    const int v = vlo + tid, xx = v + pl;
+    int a0, a1;
+    float l;
+    lin_idx(sw, v, Ws, a0, a1, l);
+    const bool ok = xx >= 0 && xx < Wp;
+    tab_i0[tid] = ok ? a0 : -1;
+    tab_i1[tid] = ok ? a1 : -1;
+    tab_l[tid] = l;
+  }
+  // phase 1: one (column, channel vector) item per thread and trip
+  const bool cok = c4 < C4;
+  const size_t rowpix = (size_t)Wp * C4;
+  const float4* base = reinterpret_cast<const float4*>(dup) + ((size_t)n * Hp + (ulo + pt)) * rowpix + c4;
+  for (int it = tid >> 4; it < nv; it += 256 / UPB_CT) {
+    const int xx = vlo + it + pl;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cok && xx >= 0 && xx < Wp) {
+      const float4* p = base + (size_t)xx * C4;
+      float4 g[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = wy[k] != 0.f ? p[(size_t)k * rowpix] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a.x = __builtin_fmaf(wy[k], g[k].x, a.x); a.y = __builtin_fmaf(wy[k], g[k].y, a.y);
+        a.z = __builtin_fmaf(wy[k], g[k].z, a.z); a.w = __builtin_fmaf(wy[k], g[k].w, a.w);
+      }
+    }
+    t[it][tid & (UPB_CT - 1)] = a;
+  }
+  __syncthreads();
+  // phase 2: one (source column, channel vector) per thread
+  const int j = j0 + (tid >> 4);
+  if (j > jlast || !cok) return;
+  const int vjlo = max(vlo, (int)ceilf((float)(j - 1) / sw) - 1), vjhi = min(vhi, (int)floorf((float)(j + 1) / sw) + 1);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int v = vjlo; v <= vjhi; ++v) {
+    const int q = v - vlo;
+    const float l = tab_l[q];
+    const float w = (tab_i0[q] == j ? 1.f - l : 0.f) + (tab_i1[q] == j ? l : 0.f);
+    const float4 g = t[q][tid & (UPB_CT - 1)];
+    a.x = __builtin_fmaf(w, g.x, a.x); a.y = __builtin_fmaf(w, g.y, a.y);
+    a.z = __builtin_fmaf(w, g.z, a.z); a.w = __builtin_fmaf(w, g.w, a.w);
+  }
+  float4* o = reinterpret_cast<float4*>(dx) + (((size_t)n * Hs + i) * Ws + j) * C4 + c4;
+  if (accum) {
+    const float4 b = *o;
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  *o = a;
+}
+
 // NHWC gather adjoint: dx[n,i,j,c] (+)= Σ_{u,v} wy(u,i) wx(v,j) d_up[n, u+pt, v+pl, c]
 __global__ void upsample_bwd_kernel(long long N, int C, int Hs, int Ws, int up_h, int up_w, int pt, int pl, int Hp,
                                     int Wp, float sh, float sw, const float* dup, float* dx, int accum) {
@@ -823,6 +916,15 @@ int unet_upsample_bwd(long long N, int C, int Hs, int Ws, int up_h, int up_w, in
   // widest destination window of upsample_bwd4w: floor(2/scale) + 3 taps (scale 0: the whole map)
   auto span = [](float sc, int up) { return sc > 0.f ? (int)floorf(2.f / sc) + 3 : up + 8; };
   if (C % 4 == 0 && span(sh, up_h) <= 8 && span(sw, up_w) <= 8) {
+    // the tiled kernel: its destination-column window for UPB_J source columns must fit the LDS table
+    const int vspan = (int)floorf((float)(UPB_J + 1) / sw) + 4;
+    const char* e = getenv("UNET_UPB_TILE");
+    const long long ntj = cdiv(Ws, UPB_J), ntc = cdiv(C / 4, UPB_CT), nblk = N * Hs * ntj * ntc;
+    if (!(e && atoi(e) == 0) && vspan <= UPB_VMAX && nblk < (1LL << 31)) {
+      hipLaunchKernelGGL(upsample_bwd_tile_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, (int)N, C, Hs,
+                         Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum, (int)ntj, (int)ntc);
+      return check_launch("upsample_bwd");
+    }
     if (total / 4 < (1LL << 31))
       hipLaunchKernelGGL(upsample_bwd4w_kernel<unsigned>, dim3(grid_for(total / 4, block_cap("UNET_UPB_BLOCKS", 8192))), dim3(256), 0, (hipStream_t)stream,
                          N, C, Hs, Ws, up_h, up_w, pad_t, pad_l, Hp, Wp, sh, sw, d_up, dx, accum);
