@@ -110,6 +110,9 @@ typedef struct unet_conv_desc {
    * attention gate, layers.py:33-34,192), op dtype [N,H,W,src[0].C], written once — the weight
    * gradient of this conv then reads a stored map instead of re-applying the transform               */
   void* act_out;
+  /* scratch of unet_conv_workspace(d) bytes (device), or NULL when that is 0: the split-K form of the 3x3
+   * conv on maps too small to fill the chip keeps its fp32 partial sums there                        */
+  void* workspace;
 } unet_conv_desc;
 
 typedef struct unet_wgrad_desc {
@@ -131,6 +134,8 @@ int unet_conv_mtiles(int N, int H, int W);
 int unet_conv_stats_rows(const unet_conv_desc* d);
 /* name of the kernel instantiation unet_conv dispatches d to (for profiling / roofline probes)   */
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len);
+/* bytes of d->workspace unet_conv needs for d (0: none)                                           */
+size_t unet_conv_workspace(const unet_conv_desc* d);
 /* does unet_conv write d->act_out for this descriptor (else the caller keeps the activation source)? */
 int unet_conv_act_out_ok(const unet_conv_desc* d);
 /* name of the weight-gradient kernel unet_conv_wgrad dispatches d to (profiling / tests)          */

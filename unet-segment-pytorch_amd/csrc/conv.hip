@@ -483,6 +483,8 @@ static int dispatch_cfg(const unet_conv_desc* d, const ConvCfg& c, hipStream_t s
 
 template <typename T> int dispatch_generic(const unet_conv_desc* d, hipStream_t st);
 bool conv5_eligible(const unet_conv_desc* d);   // conv5.hip: the LDS-DMA 3x3 path
+bool conv5_serves(const unet_conv_desc* d);     // conv5.hip: eligible, or small enough for its split-K form
+size_t conv5_workspace(const unet_conv_desc* d);
 bool conv5_act_out_ok(const unet_conv_desc* d);
 int pack_tiles_launch(int dtype, int count, const unet_pack_job* jobs, hipStream_t st);   // pack.hip
 int conv5_run(const unet_conv_desc* d, hipStream_t st);
@@ -515,7 +517,7 @@ template <typename T>
 static int dispatch_conv(const unet_conv_desc* d, hipStream_t st) {
   if (!fast_eligible(d)) return dispatch_generic<T>(d, st);
   if constexpr (sizeof(T) == 2) {
-    if (conv5_eligible(d)) return conv5_run(d, st);
+    if (conv5_serves(d)) return conv5_run(d, st);
   }
   const ConvCfg c = pick_cfg(d);
   if constexpr (sizeof(T) == 2) {
@@ -603,7 +605,7 @@ int unet_conv_mtiles(int N, int H, int W) { return N * cdiv(W, CTW) * cdiv(H, 8)
 // does unet_conv reduce d's bnb_* sums in the conv epilogue (rows = the conv's M tiles)?
 static bool bnb_in_epilogue(const unet_conv_desc* d) {
   if (smallcin_conv_ok(d) || pw_conv_ok(d) || !fast_eligible(d) || d->dtype == UNET_F32) return false;
-  if (conv5_eligible(d)) return true;
+  if (conv5_serves(d)) return true;
   return conv3_bnb_tile(d, pick_cfg(d));
 }
 
@@ -612,9 +614,14 @@ int unet_conv_stats_rows(const unet_conv_desc* d) {
   if (smallcin_conv_ok(d)) return smallcin_stats_rows(d);
   if (pw_conv_ok(d)) return pw_conv_rows(d);
   if (!fast_eligible(d)) return d->N * cdiv(d->W, CTW) * cdiv(d->H, 8);
-  if (conv5_eligible(d)) return conv5_stats_rows(d);
+  if (d->dtype != UNET_F32 && conv5_serves(d)) return conv5_stats_rows(d);
   const ConvCfg c = pick_cfg(d);
   return d->N * cdiv(d->W, CTW) * cdiv(d->H, 4 * c.wm);
+}
+
+size_t unet_conv_workspace(const unet_conv_desc* d) {
+  if (!d || smallcin_conv_ok(d) || pw_conv_ok(d) || !fast_eligible(d) || d->dtype == UNET_F32) return 0;
+  return conv5_workspace(d);
 }
 
 int unet_conv_act_out_ok(const unet_conv_desc* d) { return d && conv5_act_out_ok(d) ? 1 : 0; }
@@ -630,7 +637,7 @@ int unet_conv_variant(const unet_conv_desc* d, char* buf, int len) {
              d->Cout <= 32 ? 32 : 64);
     return 0;
   }
-  if (conv5_eligible(d)) return conv5_variant(d, buf, len);
+  if (d->dtype != UNET_F32 && conv5_serves(d)) return conv5_variant(d, buf, len);
   const ConvCfg c = pick_cfg(d);
   if (conv3_eligible(d)) {
     // the (wm, wn, ntn) block tile of pick_cfg; 16-row tiles run as MI=8 waves (dispatch_conv3)

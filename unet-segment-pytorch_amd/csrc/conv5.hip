@@ -75,9 +75,12 @@ struct C5Layout {
 // channels); 4 = 4 row groups, each wave all 64 channels (one wave per SIMD with the whole 512-register file:
 // every halo fragment it reads from LDS feeds twice the MFMAs — 12 reads per 24 MFMAs per tap column instead
 // of 9 per 12 — and the two accumulator halves and both operand columns fit without spills)
-template <typename T, int MI, int OM, int SK, int GATE, int ABL = 0, int PIPE = 1, int NWV = 8>
+// SPLIT (round 5, maps too small to fill the chip): blockIdx.z owns the 16-channel chunks [z*nch, (z+1)*nch) of
+// the nch_all in the reduction and writes its fp32 partial sums to slab z of d.out ([S][N*H*W][Cout], OM5_F32,
+// split == Cout, no accumulation: the host's descriptor); conv5_splitk_finish_kernel sums the slabs in order
+template <typename T, int MI, int OM, int SK, int GATE, int ABL = 0, int PIPE = 1, int NWV = 8, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc d, int tiles_w, int tiles_h,
-                                                           int mtiles, int nch) {
+                                                           int mtiles, int nch, int nch_all) {
   using F = typename Mma32<T>::frag;
   constexpr bool ACT = SK != SK_PLAIN;
   constexpr int WN = NWV / C5_WM, NJ = C5_WH / WN, NT = 64 * NWV;
@@ -114,7 +117,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   const float lo = s0.relu ? 0.f : -INFINITY;
 
   // ---- weights: A fragment (32 output channels x 16 k) of the 16x16x32 fragment-major packing ----
-  const int nch32 = (nch + 1) >> 1;
+  const int nch32 = (nch_all + 1) >> 1;
+  const int kc0 = SPLIT ? (int)blockIdx.z * nch : 0;   // this block's first chunk of the reduction
   const unsigned jstride = (unsigned)nch32 * 9u * 1024u;
   const unsigned ntiles16 = (unsigned)((d.Cout + C5_NPAD - 1) / C5_NPAD * (C5_NPAD / 16));
   const rsrc4_t rw = mk_rsrc4(d.weight, ntiles16 * jstride);
@@ -203,7 +207,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   // pre-activations of this lane's slots (returns whether those went out: the chunk counts ND + DPW)
   auto issue = [&](const Cur& q, bool prologue) -> bool {
     if (q.c == 0) tile_slots(q, ib0, ib1);
-    const int cn0 = q.c * 16;
+    const int ca = q.c + kc0;                       // the chunk's index in the whole reduction
+    const int cn0 = ca * 16;
     const bool s1sel = d.nsrc > 1 && cn0 >= C0;
     const int cl = s1sel ? cn0 - C0 : cn0;
     const int Cs = s1sel ? s1.C : C0;
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
     }
     if (!(ABL & 2) || prologue) {
       const unsigned wd = l32 + Lay::OFF_W + q.s3 * Lay::WIMG;
-      const unsigned wofs = (unsigned)((q.c >> 1) * 9) * 1024u + (unsigned)(q.c & 1) * 512u;
+      const unsigned wofs = (unsigned)((ca >> 1) * 9) * 1024u + (unsigned)(ca & 1) * 512u;
 #pragma unroll
       for (int k = 0; k < WPW; ++k) {
         const int j = wave + k * NWV;
@@ -269,7 +274,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
         xao[k] = in ? (pix * (unsigned)C0 + 8u * hbit[k]) * 2u : OOB;
       }
     }
-    const int cn0 = q.c * 16;
+    const int cn0 = (q.c + kc0) * 16;
     // src0 (activation) or, for SK_ACT_PLAIN, src1 (stored: copied)
     const bool act = SK == SK_ACT || !(d.nsrc > 1 && cn0 >= C0);
     const bool rag = cn0 + 16 > C0;
@@ -401,7 +406,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   // F32 without accumulation: counted buffer stores (no RMW loads, whose compiler waits drain the DMA queue)
   const bool f32_counted = OM == OM5_F32 && !d.accum && !d.accum2 && (d.split % 8) == 0 &&
                            (double)npix * d.Cout * 4 < (double)OOB;
-  const rsrc_t rf1 = mk_rsrc(d.out, (unsigned)(f32_counted ? npix * d.split * 4 : 0));
+  const rsrc_t rf1 = mk_rsrc(SPLIT ? (const void*)((const char*)d.out + (size_t)blockIdx.z * (size_t)npix * d.Cout * 4) : d.out,
+                             (unsigned)(f32_counted ? npix * d.split * 4 : 0));
   const rsrc_t rf2 = mk_rsrc(d.out2 ? d.out2 : d.out, (unsigned)(f32_counted ? npix * (d.Cout - d.split) * 4 : 0));
   constexpr int NYL = OM == OM5_BNB ? 4 * MI * NJ : 0;
   int sw = 0;
@@ -741,6 +747,103 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
 }
 
 // ------------------------------------------------------------------------------------------------
+// split-K finisher: out = sum over the S slabs of ws ([S][npix][Cout] fp32, in slab order) through the conv's
+// real epilogue.  Block = CV = Cout/4 channel vectors x R = 256/CV pixel lanes over a contiguous pixel range
+// (one partial-sum row per block, like one conv5 workgroup row).  MODE 0: y (op dtype) + the BN partial sums of
+// the fp32 sums (stats[2][Cout][rows], as conv5's y epilogue sums its accumulators); 1: y + the BatchNorm-backward
+// sums of the stored gradient (bnb_stats[2][rows][Cout], conv5's OM5_BNB); 2: fp32, split across out / out2,
+// optionally accumulating
+// ------------------------------------------------------------------------------------------------
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void conv5_splitk_finish_kernel(const unet_conv_desc d, const float* __restrict__ ws,
+                                                                  int S, int rows) {
+  __shared__ float4 red[2][256];
+  const int CV = d.Cout >> 2, R = 256 / CV, tid = threadIdx.x;
+  const int cv = tid % CV, r = tid / CV, co = cv * 4;
+  const long long npix = (long long)d.N * d.H * d.W;
+  const long long per = (npix + rows - 1) / rows;
+  const long long p0 = (long long)blockIdx.x * per, p1 = min(npix, p0 + per);
+  const size_t slab = (size_t)npix * d.Cout;
+  float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), sb = sa;
+  float4 sc = sa, sf = sa;
+  if constexpr (MODE == 1) {
+    if (d.bnb_relu) {
+      sc = *reinterpret_cast<const float4*>(d.bnb_scale + co);
+      sf = *reinterpret_cast<const float4*>(d.bnb_shift + co);
+    }
+  }
+  for (long long p = p0 + r; p < p1; p += R) {
+    const float4* src = reinterpret_cast<const float4*>(ws + (size_t)p * d.Cout + co);
+    float4 v = src[0];
+    for (int z = 1; z < S; ++z) {
+      const float4 q = src[(size_t)z * (slab / 4)];
+      v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+    }
+    if constexpr (MODE == 0 || MODE == 1) {
+      uint2 pk;
+      pk.x = pack2_16<T>(v.x, v.y);
+      pk.y = pack2_16<T>(v.z, v.w);
+      *reinterpret_cast<uint2*>((T*)d.out + (size_t)p * d.Cout + co) = pk;
+      if constexpr (MODE == 0) {
+        sa.x += v.x; sa.y += v.y; sa.z += v.z; sa.w += v.w;
+        sb.x = __builtin_fmaf(v.x, v.x, sb.x); sb.y = __builtin_fmaf(v.y, v.y, sb.y);
+        sb.z = __builtin_fmaf(v.z, v.z, sb.z); sb.w = __builtin_fmaf(v.w, v.w, sb.w);
+      } else {
+        float g[4], y[4];
+        unpack4_16<T>(pk, g);
+        unpack4_16<T>(*reinterpret_cast<const uint2*>((const T*)d.bnb_y + (size_t)p * d.Cout + co), y);
+        const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, sfv[4] = {sf.x, sf.y, sf.z, sf.w};
+        float gg[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gg[k] = (d.bnb_relu && !(y[k] * scv[k] + sfv[k] > 0.f)) ? 0.f : g[k];
+        sa.x += gg[0]; sa.y += gg[1]; sa.z += gg[2]; sa.w += gg[3];
+        sb.x = __builtin_fmaf(gg[0], y[0], sb.x); sb.y = __builtin_fmaf(gg[1], y[1], sb.y);
+        sb.z = __builtin_fmaf(gg[2], y[2], sb.z); sb.w = __builtin_fmaf(gg[3], y[3], sb.w);
+      }
+    } else {
+      float4* o;
+      int acc;
+      if (co < d.split) { o = reinterpret_cast<float4*>((float*)d.out + (size_t)p * d.split + co); acc = d.accum; }
+      else { o = reinterpret_cast<float4*>((float*)d.out2 + (size_t)p * (d.Cout - d.split) + (co - d.split)); acc = d.accum2; }
+      if (acc) {
+        const float4 b = *o;
+        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+      }
+      *o = v;
+    }
+  }
+  if constexpr (MODE == 0 || MODE == 1) {
+    if (MODE == 0 && !d.stats) return;
+    red[0][tid] = sa;
+    red[1][tid] = sb;
+    __syncthreads();
+    if (r == 0) {
+      float4 a = red[0][cv], b = red[1][cv];
+      for (int k = 1; k < R; ++k) {
+        const float4 x = red[0][k * CV + cv], y = red[1][k * CV + cv];
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+        b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+      }
+      if constexpr (MODE == 0) {
+        const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d.stats[(size_t)(co + k) * rows + blockIdx.x] = av[k];
+          d.stats[(size_t)(d.Cout + co + k) * rows + blockIdx.x] = bv[k];
+        }
+      } else {
+        const float4 m4 = *reinterpret_cast<const float4*>(d.bnb_mean + co);
+        const float4 i4 = *reinterpret_cast<const float4*>(d.bnb_invstd + co);
+        b = make_float4(i4.x * (b.x - m4.x * a.x), i4.y * (b.y - m4.y * a.y), i4.z * (b.z - m4.z * a.z),
+                        i4.w * (b.w - m4.w * a.w));
+        *reinterpret_cast<float4*>(d.bnb_stats + (size_t)blockIdx.x * d.Cout + co) = a;
+        *reinterpret_cast<float4*>(d.bnb_stats + ((size_t)rows + blockIdx.x) * d.Cout + co) = b;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
 constexpr int C5_MI = 4;
@@ -768,13 +871,7 @@ static int conv5_gx(const unet_conv_desc* d) {
 // 16-bit 3x3; stored or BN-activation sources (src0 may be gated, src1 stored; the network's pooled and
 // upsampled maps are materialised), Cin > 16 (two chunks in flight), a BN activation of <= 1024 channels,
 // y / y + BN-backward sums / fp32 epilogues, enough 16 x 32 tiles to fill the chip
-bool conv5_eligible(const unet_conv_desc* d) {
-  const int mode = conv5_mode();
-  if (mode == 0) return false;
-  // default: every 16-bit y output (forward and the middle-activation dgrads) and the fp32 dgrads of <= 64
-  // channels — per layer conv5 measured 0-31 % faster there (the 512^2 64-channel layers 14-31 %); the
-  // wider fp32 dgrads stay on conv3, whose tiles measured 5-20 % faster (profiles/r03_layerprof_*.txt)
-  if (mode == 2 && d->out_mode == UNET_OUT_F32 && d->Cout > C5_BN) return false;
+static bool conv5_shape_ok(const unet_conv_desc* d) {
   if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 3) return false;
   if (d->out_mode != UNET_OUT_Y && d->out_mode != UNET_OUT_F32) return false;
   if (d->Cout % 8 || (d->out_mode == UNET_OUT_F32 && d->split % 4)) return false;   // 16-byte y stores
@@ -792,11 +889,59 @@ bool conv5_eligible(const unet_conv_desc* d) {
   }
   if ((double)d->N * d->H * d->W * 4 >= (double)OOB) return false;
   if ((double)d->N * d->H * d->W * d->Cout * 2 >= (double)OOB) return false;   // y stores: OOB masks lanes
+  return true;
+}
+
+bool conv5_eligible(const unet_conv_desc* d) {
+  const int mode = conv5_mode();
+  if (mode == 0) return false;
+  // default: every 16-bit y output (forward and the middle-activation dgrads) and the fp32 dgrads of <= 64
+  // channels — per layer conv5 measured 0-31 % faster there (the 512^2 64-channel layers 14-31 %); the
+  // wider fp32 dgrads stay on conv3, whose tiles measured 5-20 % faster (profiles/r03_layerprof_*.txt)
+  if (mode == 2 && d->out_mode == UNET_OUT_F32 && d->Cout > C5_BN) return false;
+  if (!conv5_shape_ok(d)) return false;
   const long long work = conv5_mtiles(d) * cdiv(d->Cout, C5_BN);
   return work >= 256;
 }
 
-int conv5_stats_rows(const unet_conv_desc* d) { return conv5_gx(d) * C5_WM; }
+// ---- split-K over the input channels for maps whose 16 x 32 x 64 tiles do not fill the chip (round 5,
+// the 32^2 512 -> 512 down4 layers ran on conv3 at 12-15 % of peak with 64 tiles of work):
+// S = the smallest power of two with tiles x S >= 256 (<= 8), each split >= 2 chunks; the partial sums go to
+// S fp32 slabs in d->workspace and conv5_splitk_finish_kernel adds them in slab order (deterministic) and applies
+// the real epilogue (y + BN partial sums, y + BN-backward sums, or fp32 with split / accumulation).
+// UNET_CONV5_SPLIT=0 turns it off (A/B).
+int conv5_splitk(const unet_conv_desc* d) {
+  static const int on = [] { const char* e = getenv("UNET_CONV5_SPLIT"); return e ? atoi(e) : 1; }();
+  if (!on || conv5_mode() == 0 || d->act_out || !conv5_shape_ok(d)) return 1;
+  if (d->Cout > 1024 || (d->Cout & (d->Cout - 1))) return 1;     // the finisher's channel-vector layout
+  const long long work = conv5_mtiles(d) * cdiv(d->Cout, C5_BN);
+  if (work >= 256) return 1;
+  const int nch = cdiv(d->Cin, 16);
+  int S = 1;
+  while (work * S < 256 && S < 8 && nch % (2 * S) == 0 && nch / (2 * S) >= 2) S *= 2;
+  return S;
+}
+
+bool conv5_serves(const unet_conv_desc* d) { return conv5_eligible(d) || conv5_splitk(d) > 1; }
+
+size_t conv5_workspace(const unet_conv_desc* d) {
+  const int S = conv5_eligible(d) ? 1 : conv5_splitk(d);
+  return S > 1 ? (size_t)S * d->N * d->H * d->W * d->Cout * sizeof(float) : 0;
+}
+
+// the finisher: 256 threads = CV channel vectors (4 channels) x R pixel lanes, FIN_TRIPS pixels per lane
+constexpr int FIN_TRIPS = 8;
+static int fin_rows(const unet_conv_desc* d) {
+  const int R = 256 / (d->Cout / 4);
+  const long long npix = (long long)d->N * d->H * d->W;
+  long long rows = (npix + (long long)R * FIN_TRIPS - 1) / ((long long)R * FIN_TRIPS);
+  return (int)(rows < 1 ? 1 : rows);
+}
+
+int conv5_stats_rows(const unet_conv_desc* d) {
+  if (!conv5_eligible(d) && conv5_splitk(d) > 1) return fin_rows(d);
+  return conv5_gx(d) * C5_WM;
+}
 
 // can the forward write src[0]'s transformed input to act_out (the y-mode BN-activation kernel serves d)?
 bool conv5_act_out_ok(const unet_conv_desc* d) {
@@ -805,7 +950,9 @@ bool conv5_act_out_ok(const unet_conv_desc* d) {
 }
 
 int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
-  snprintf(buf, len, "conv5_kernel<%s,%d>", d->dtype == UNET_F16 ? "fp16" : "bf16", C5_MI);
+  const int S = conv5_eligible(d) ? 1 : conv5_splitk(d);
+  if (S > 1) snprintf(buf, len, "conv5_kernel<%s,%d>+splitk%d", d->dtype == UNET_F16 ? "fp16" : "bf16", C5_MI, S);
+  else snprintf(buf, len, "conv5_kernel<%s,%d>", d->dtype == UNET_F16 ? "fp16" : "bf16", C5_MI);
   return 0;
 }
 
@@ -824,9 +971,45 @@ static int launch5(const unet_conv_desc* d, hipStream_t st) {
   const int mt = d->N * tw * th;
   const int gy = cdiv(d->Cout, C5_BN);
   const int gx = conv5_gx(d);
+  const int nch = cdiv(d->Cin, 16);
   hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, PIPE, 8>), dim3(gx, gy), dim3(512), 0, st, *d, tw, th,
-                     mt, cdiv(d->Cin, 16));
+                     mt, nch, nch);
   return check_launch("conv5");
+}
+
+// split-K: the conv into S fp32 slabs (one workgroup per tile and split), then the finisher
+template <typename T, int SK, int GATE>
+static int launch5_split(const unet_conv_desc* d, int S, hipStream_t st) {
+  constexpr int TH = C5_WM * C5_MI;
+  if (!d->workspace) {
+    set_error("unet_conv: this descriptor runs split-K and needs d->workspace (unet_conv_workspace bytes)");
+    return UNET_ERR_ARG;
+  }
+  const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH);
+  const int mt = d->N * tw * th;
+  const int gy = cdiv(d->Cout, C5_BN);
+  const int nch = cdiv(d->Cin, 16);
+  unet_conv_desc k = *d;
+  k.out_mode = UNET_OUT_F32;
+  k.out = d->workspace;
+  k.out2 = nullptr;
+  k.split = d->Cout;
+  k.accum = k.accum2 = 0;
+  k.stats = nullptr;
+  k.bnb_stats = nullptr;
+  k.act_out = nullptr;
+  hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM5_F32, SK, GATE, 0, 1, 8, true>), dim3(mt, gy, S), dim3(512), 0, st, k,
+                     tw, th, mt, nch / S, nch);
+  if (int e = check_launch("conv5 split")) return e;
+  const int rows = fin_rows(d);
+  const float* ws = (const float*)d->workspace;
+  if (d->out_mode == UNET_OUT_F32)
+    hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, 2>), dim3(rows), dim3(256), 0, st, *d, ws, S, rows);
+  else if (d->bnb_stats)
+    hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, 1>), dim3(rows), dim3(256), 0, st, *d, ws, S, rows);
+  else
+    hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, 0>), dim3(rows), dim3(256), 0, st, *d, ws, S, rows);
+  return check_launch("conv5 split finish");
 }
 
 // source kind of a descriptor: plain, one BN activation (gated or not), or a BN activation + a stored map.
@@ -844,6 +1027,12 @@ static int dispatch5_om(const unet_conv_desc* d, hipStream_t st) {
 
 template <typename T>
 static int dispatch5(const unet_conv_desc* d, hipStream_t st) {
+  if (!conv5_eligible(d)) {
+    const int S = conv5_splitk(d);
+    const unet_src& s0 = d->src[0];
+    if (s0.kind != UNET_SRC_ACT) return launch5_split<T, SK_PLAIN, 0>(d, S, st);
+    return s0.gate_p ? launch5_split<T, SK_ACT_PLAIN, 1>(d, S, st) : launch5_split<T, SK_ACT_PLAIN, 0>(d, S, st);
+  }
   if (d->out_mode == UNET_OUT_F32) return dispatch5_om<T, OM5_F32>(d, st);
   if (d->bnb_stats) return dispatch5_om<T, OM5_BNB>(d, st);
   return dispatch5_om<T, OM5_Y>(d, st);

@@ -540,7 +540,9 @@ bool pw_conv_ok(const unet_conv_desc* d) {
   if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 1 || d->nsrc != 1 ||
       !pw_src_ok(d->src[0], d->Cin))
     return false;
-  if (d->Cin % 32 || d->Cout % 16 || d->Cin > 256 || P < 32768) return false;
+  static const int wide = [] { const char* e = getenv("UNET_PW_WIDE"); return e ? atoi(e) : 0; }();
+  if (d->Cin % 32 || d->Cout % 16) return false;
+  if (wide ? (d->Cin > 512 || P < 16384) : (d->Cin > 256 || P < 32768)) return false;
   if (d->out_mode == UNET_OUT_F32) { if (d->split % 4) return false; }
   else if (d->out_mode == UNET_OUT_F32_GATED) { if (d->split != d->Cout) return false; }
   else if (d->out_mode != UNET_OUT_Y) return false;

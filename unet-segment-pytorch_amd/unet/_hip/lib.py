@@ -33,7 +33,7 @@ class ConvDesc(ctypes.Structure):
                 ("out", c_vp), ("out2", c_vp), ("split", c_int), ("accum", c_int), ("accum2", c_int),
                 ("stats", c_vp), ("pool_src", Src), ("bias", c_vp), ("pool_code", c_vp),
                 ("bnb_y", c_vp), ("bnb_scale", c_vp), ("bnb_shift", c_vp), ("bnb_relu", c_int), ("bnb_mean", c_vp),
-                ("bnb_invstd", c_vp), ("bnb_stats", c_vp), ("act_out", c_vp)]
+                ("bnb_invstd", c_vp), ("bnb_stats", c_vp), ("act_out", c_vp), ("workspace", c_vp)]
 
 
 class PackJob(ctypes.Structure):
@@ -58,6 +58,7 @@ _SIGS = {
     "unet_conv_variant": (c_int, [ctypes.POINTER(ConvDesc), ctypes.c_char_p, c_int]),
     "unet_wgrad_variant": (c_int, [ctypes.POINTER(WgradDesc), ctypes.c_char_p, c_int]),
     "unet_conv_act_out_ok": (c_int, [ctypes.POINTER(ConvDesc)]),
+    "unet_conv_workspace": (c_size, [ctypes.POINTER(ConvDesc)]),
     "unet_pack_weight": (c_int, [c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "unet_packed_weight_elems": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "unet_pack_weights": (c_int, [c_int, c_int, ctypes.POINTER(PackJob), c_vp]),
@@ -139,7 +140,7 @@ _GUARD = os.environ.get("UNET_GUARD", "") not in ("", "0")
 _guard = None
 # queries that launch nothing
 _NO_LAUNCH = {"unet_last_error", "unet_version", "unet_conv_mtiles", "unet_conv_stats_rows", "unet_conv_variant",
-              "unet_wgrad_variant", "unet_conv_act_out_ok", "unet_packed_weight_elems", "unet_wgrad_workspace",
+              "unet_wgrad_variant", "unet_conv_act_out_ok", "unet_conv_workspace", "unet_packed_weight_elems", "unet_wgrad_workspace",
               "unet_bn_bwd_reduce_rows", "unet_gate_psi_rows", "unet_gate_bwd2_rows", "unet_convt_bwd_rows",
               "unet_outconv_rows", "unet_loss_rows"}
 
@@ -229,6 +230,19 @@ def check(rc: int, what: str):
 
 def call(name: str, *args):
     lib = load()
+    if name == "unet_conv" and not args[0].workspace:
+        # the split-K form of a small-map 3x3 conv needs scratch for its fp32 partial sums: allocated here from
+        # torch's caching allocator on the current stream (valid for the kernels enqueued below)
+        n = lib.unet_conv_workspace(args[0])
+        if n:
+            ws = torch.empty(n, dtype=torch.uint8, device="cuda")
+            args[0].workspace = ws.data_ptr()
+            try:
+                rc = lib.unet_conv(*args)
+            finally:
+                args[0].workspace = None
+            check(rc, name)
+            return rc
     rc = getattr(lib, name)(*args)
     check(rc, name)
     return rc
