@@ -43,7 +43,8 @@ def _conv_kinds(log):
 
 def _assert_16bit_paths(log, prec):
     """every conv of a 16-bit run is on a 16-bit MFMA kernel (no generic fallback; conv2 only for the small-map
-    1x1 projections); the 64-channel 3x3 y outputs (mode 0) ran on conv5 (csrc/conv5.hip) and the fp32
+    1x1 projections); the 64-channel 3x3 y outputs (mode 0) ran on conv5 (csrc/conv5.hip), the small-map ones on its
+    split-K form, and the fp32
     dgrads (mode 1) on the 16-bit conv3 / conv5 tiles — the bench's kernels under the default policy"""
     names = _conv_kinds(log)
     bad = [n for n in names if n.startswith(("conv_generic", "conv2_kernel<fp32")) or (n.startswith("conv2_kernel")
@@ -52,7 +53,9 @@ def _assert_16bit_paths(log, prec):
     assert any(n.startswith(f"conv5_kernel<{prec},") and m == 0 for n, m in log), sorted(names)
     assert any(n.startswith((f"conv5_kernel<{prec},", f"conv3_kernel<{prec},3,")) and m == 1 for n, m in log), \
         sorted(names)
-    assert any(n.startswith(f"conv3_kernel<{prec},3,") and m == 0 for n, m in log), sorted(names)
+    # the small-map y outputs (down4 at 32^2, up1.conv.3 at 64^2): conv5's split-K form since round 5 (conv3 before)
+    assert any((n.startswith(f"conv5_kernel<{prec},") and "+splitk" in n or n.startswith(f"conv3_kernel<{prec},3,"))
+               and m == 0 for n, m in log), sorted(names)
     return names
 
 

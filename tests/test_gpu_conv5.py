@@ -138,3 +138,97 @@ def test_conv5_matches_conv3(prec, path, monkeypatch):
     assert v4.startswith(f"{path}_kernel") and v3.startswith("conv3_kernel"), (v4, v3)
     rel = float((o4 - o3).double().norm() / o3.double().norm())
     assert rel <= 1e-5, rel
+
+
+# ---- split-K (round 5): maps whose 16 x 32 x 64 tiles do not fill the chip (down4 at 32^2, up1.conv.3 at 64^2) ----
+SPLIT_SHAPES = [(4, 32, 32, 512, 512), (4, 64, 64, 512, 256), (2, 16, 16, 256, 128), (2, 16, 24, 64, 64)]
+
+
+@pytest.mark.parametrize("shape", SPLIT_SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("src", ["plain", "act", "act_gate", "concat"])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv5_splitk_y_stats(prec, src, shape):
+    """The split-K form against torch fp32 on the same operands: y and the BN partial sums (same gates as the
+    persistent form), and bit-identical across two runs (the slabs are added in a fixed order)."""
+    L, R = _lib(), _rt()
+    N, H, W, cin, cout = shape
+    dt = DT[prec]
+    torch.manual_seed(41)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
+    if src == "concat":
+        c0 = cin // 2
+        y0 = _rand(N, H, W, c0, dt=dt)
+        ab0 = torch.stack([torch.rand(c0, device="cuda") + 0.5, torch.randn(c0, device="cuda") * 0.2])
+        up = _rand(N, H, W, cin - c0, dt=dt)
+        s1 = L.Src()
+        s1.kind, s1.C, s1.H, s1.W, s1.data = L.SRC_PLAIN, cin - c0, H, W, up.data_ptr()
+        srcs = [_act_src(y0, ab0), s1]
+        x = torch.cat([_act_ref(y0, ab0).to(dt).float(), up.float()], -1)
+    else:
+        y = _rand(N, H, W, cin, dt=dt)
+        if src == "plain":
+            s = L.Src()
+            s.kind, s.C, s.H, s.W, s.data = L.SRC_PLAIN, cin, H, W, y.data_ptr()
+            x = y.float()
+        else:
+            ab = torch.stack([torch.rand(cin, device="cuda") + 0.5, torch.randn(cin, device="cuda") * 0.2])
+            s = _act_src(y, ab)
+            a = _act_ref(y, ab)
+            if src == "act_gate":
+                p = torch.randn(N, H, W, device="cuda")
+                pab = torch.tensor([0.7, -0.1], device="cuda")
+                s.gate_p, s.gate_ab = p.data_ptr(), pab.data_ptr()
+                a = a * torch.sigmoid(p * 0.7 - 0.1)[..., None]
+            x = a.to(dt).float()
+        srcs = [s]
+    d0 = L.ConvDesc()
+    d0.dtype, d0.N, d0.H, d0.W, d0.Cin, d0.Cout, d0.ksize, d0.nsrc = R._PRECISIONS[prec].code, N, H, W, cin, cout, 3, len(srcs)
+    for i, s in enumerate(srcs):
+        d0.src[i] = s
+    rows = L.load().unet_conv_stats_rows(d0)
+    outs = []
+    for _ in range(2):
+        st = torch.full((2, cout, rows), float("nan"), device="cuda")
+        out = torch.full((N, H, W, cout), float("nan"), dtype=dt, device="cuda")
+        d = _conv(prec, srcs, N, H, W, cin, w, 3, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
+        outs.append((out, st))
+    v = _variant(d)
+    assert v.startswith(f"conv5_kernel<{TN[prec]},4>+splitk"), v
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])   # deterministic
+    out, st = outs[0]
+    ref = F.conv2d(x.permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
+    _close_bf16(out.float(), ref, "y")
+    r = ref.double().reshape(-1, cout)
+    sm = st.double().sum(-1)
+    assert torch.isfinite(sm).all()
+    assert ((sm[0] - r.sum(0)).abs() <= 1e-3 * r.abs().sum(0) + 1e-2).all()
+    assert ((sm[1] - (r * r).sum(0)).abs() <= 1e-2 * (r * r).sum(0) + 1e-2).all()
+
+
+SPLIT_DGRAD_SHAPES = [(4, 32, 32, 512, 512), (4, 32, 32, 256, 512), (2, 16, 16, 256, 128), (2, 16, 24, 64, 64)]
+
+
+@pytest.mark.parametrize("shape", SPLIT_DGRAD_SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv5_splitk_dgrad_f32_split_accum(prec, shape):
+    """The split-K fp32 dgrad epilogue: split across the concat, the first part accumulated, and unsplit."""
+    L = _lib()
+    N, H, W, cin, cout = shape
+    dt = DT[prec]
+    torch.manual_seed(42)
+    dy = _rand(N, H, W, cout, dt=dt)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
+    ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    split = cin // 2
+    o1 = torch.full((N, H, W, split), 0.5, device="cuda")
+    o2 = torch.full((N, H, W, cin - split), float("nan"), device="cuda")
+    d = _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
+              split=split, accum=1, accum2=0)
+    v = _variant(d)
+    assert "+splitk" in v, v
+    _close_bf16(torch.cat([o1 - 0.5, o2], -1), ref, "dgrad f32")
+    o = torch.full((N, H, W, cin), float("nan"), device="cuda")
+    _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o.data_ptr(), split=cin)
+    _close_bf16(o, ref, "dgrad f32 stored")

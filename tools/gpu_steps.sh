@@ -14,7 +14,7 @@ for step in ${STEPS:-tests smoke bench}; do
       || { grep -E "FAILED|Error|passed|failed" $O/gpu_tests.log | tail -20; fail tests $O/gpu_tests.log 60; }
     grep -E "passed|failed" $O/gpu_tests.log | tail -2 ;;
   some)    # a subset: PYARGS selects
-    env ${PYENV} timeout -k 10 ${TLIM:-900} python -u -m pytest -m gpu -x -v --timeout 400 --timeout-method thread --durations=20 ${PYARGS} > $O/some_tests.log 2>&1 \
+    env ${PYENV} timeout -k 10 ${TLIM:-900} python -u -m pytest -m gpu -x -v --timeout 400 --timeout-method thread --durations=20 ${PYARGS} ${PYK:+-k "$PYK"} > $O/some_tests.log 2>&1 \
       || fail some $O/some_tests.log 60
     grep -E "passed|failed" $O/some_tests.log | tail -2 ;;
   smoke)

@@ -21,3 +21,16 @@ tot = sum(r[2] for r in rows)
 for name, calls, ns in sorted(rows, key=lambda r: -r[2])[:top]:
     print(f"{ns/1e6/steps:8.3f} ms/step {100*ns/tot:6.2f}% n/step={calls/steps:6.1f} avg={ns/calls/1e3:8.1f}us  {name[:100]}")
 print(f"total {tot/1e6/steps:.2f} ms/step")
+# optional family summary: argv[4] = regex of the family's launch kernels, argv[5] = regex of companion kernels
+# whose time belongs to those launches (the split-K finisher of conv5's small-map form): avg = (family +
+# companion time) / family launches — what bench.py's probe (HIP events around the whole unet_conv call) measures
+if len(sys.argv) > 4:
+    import re
+    fam = re.compile(sys.argv[4])
+    comp = re.compile(sys.argv[5]) if len(sys.argv) > 5 else None
+    n = sum(c for nm, c, _ in rows if fam.search(nm))
+    t_f = sum(ns for nm, _, ns in rows if fam.search(nm))
+    t_c = sum(ns for nm, _, ns in rows if comp and comp.search(nm) and not fam.search(nm))
+    if n:
+        print(f"family /{sys.argv[4]}/: {n / steps:.1f} launches/step, {t_f / 1e6 / steps:.3f} ms/step"
+              f" + companions {t_c / 1e6 / steps:.3f} ms/step; avg {(t_f + t_c) / n / 1e3:.2f} us per launch")

@@ -43,6 +43,10 @@ constexpr int C5_CMAX = 1024;            // largest BN-activation source (scale 
 constexpr int C5_TABS = C5_CMAX + 8;     // table stride: each half carries its own 8-float zero pad
 constexpr int C5_NPAD = PACK_NPAD;       // packed weight rows are padded to this (conv_common.h)
 constexpr int OM5_Y = 0, OM5_F32 = 1, OM5_BNB = 2;
+// conv5's own source kind beside conv_src16.h's: one stored source whose channel count is a multiple of 16 (the
+// dgrads' dy, the Down blocks' pooled map).  Like SK_ACT (one BN activation, host-checked C % 16 == 0), it lets
+// the chunk DMA and transform drop the per-chunk source selection and ragged-chunk masks (round 5)
+constexpr int SK5_PLAIN1 = 4;
 
 template <int MI, bool ACT, int NWV>
 struct C5Layout {
@@ -82,7 +86,8 @@ template <typename T, int MI, int OM, int SK, int GATE, int ABL = 0, int PIPE = 
 __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc d, int tiles_w, int tiles_h,
                                                            int mtiles, int nch, int nch_all) {
   using F = typename Mma32<T>::frag;
-  constexpr bool ACT = SK != SK_PLAIN;
+  constexpr bool ACT = SK != SK_PLAIN && SK != SK5_PLAIN1;
+  constexpr bool ONE = SK == SK_ACT || SK == SK5_PLAIN1;   // one source, no ragged 16-channel chunk
   constexpr int WN = NWV / C5_WM, NJ = C5_WH / WN, NT = 64 * NWV;
   using Lay = C5Layout<MI, ACT, NWV>;
   constexpr int TH = Lay::TH, NS = Lay::NS, NI = Lay::NI, DPW = Lay::DPW, WPW = Lay::WPW;
@@ -94,14 +99,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   const int cw0 = blockIdx.y * C5_BN + wn * 32;     // this wave's first output channel (NJ blocks of 32)
   const int ntl = (mtiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;   // tiles of this block
   const int G = ntl * nch;                          // chunk steps of this block
-  auto tile_of = [&](int ti, int& n_, int& h0_, int& w0_) {
-    const int t = (int)blockIdx.x + ti * (int)gridDim.x;
-    const int tw_i = t % tiles_w;
-    const int t2 = t / tiles_w;
-    h0_ = (t2 % tiles_h) * TH;
-    w0_ = tw_i * C5_W;
-    n_ = t2 / tiles_h;
-  };
+  // a block's tiles are blockIdx.x + ti * gridDim.x: the first one by division, each next one by adding the
+  // grid stride's (image, tile row, tile column) decomposition with carries (round 5: the signed divisions at
+  // every tile change of three cursors were ~120 SALU per tile, paid over as few as 4 chunks on 64-channel maps)
+  const int dW = (int)(gridDim.x % (unsigned)tiles_w), dT = (int)(gridDim.x / (unsigned)tiles_w);
+  const int dH = dT % tiles_h, dN = dT / tiles_h;
 
   // ---- sources ----
   const unet_src& s0 = d.src[0];
@@ -139,7 +141,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   for (int k = 0; k < DPW; ++k) {
     const int i = wave + k * NWV, s = i * 64 + lane;
     const int hp = s >> 1;
-    hbit[k] = (s & 1) ^ ((hp >> 3) & 1);
+    // = (lane & 1) ^ ((lane >> 4) & 1) for every k and wave (s and hp move by multiples of 512 / 256 with k,
+    // 64 / 32 with the wave): written in that form so the compiler sees one value (one scale / shift read per chunk)
+    hbit[k] = (lane & 1) ^ ((lane >> 4) & 1);
+    (void)hp;
     soy[k] = s < NS ? hp / C5_HW - 1 : -(1 << 20);    // past the image: never a valid row
     sox[k] = hp % C5_HW - 1;
   }
@@ -170,18 +175,33 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
 
   // a chunk cursor: tile ti (origin n, h0, w0), 16-channel chunk c, ring slots of chunk index g
   struct Cur {
-    int ti, c, n, h0, w0, s3, s2;
+    int ti, c, n, h0, w0, s3, s2, tw, th;
   };
   auto cur_init = [&](Cur& q) {
     q.ti = 0; q.c = 0; q.s3 = 0; q.s2 = 0;
-    tile_of(0, q.n, q.h0, q.w0);
+    const unsigned t = blockIdx.x, t2 = t / (unsigned)tiles_w;
+    q.tw = (int)(t - t2 * (unsigned)tiles_w);
+    q.th = (int)(t2 % (unsigned)tiles_h);
+    q.n = (int)(t2 / (unsigned)tiles_h);
+    q.h0 = q.th * TH;
+    q.w0 = q.tw * C5_W;
   };
   auto cur_next = [&](Cur& q) {
     q.s3 = q.s3 == 2 ? 0 : q.s3 + 1;
     q.s2 ^= 1;
     if (++q.c == nch) {
       q.c = 0;
-      if (++q.ti < ntl) tile_of(q.ti, q.n, q.h0, q.w0);
+      if (++q.ti < ntl) {
+        q.tw += dW;
+        int cy = q.tw >= tiles_w;
+        q.tw -= cy ? tiles_w : 0;
+        q.th += dH + cy;
+        cy = q.th >= tiles_h;
+        q.th -= cy ? tiles_h : 0;
+        q.n += dN + cy;
+        q.h0 = q.th * TH;
+        q.w0 = q.tw * C5_W;
+      }
     }
   };
 
@@ -191,6 +211,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   // cursor: the slot's pixel inside the image / its act_out byte offset (interior pixels only, else >= OOB)
   unsigned ib0[DPW], ib1[DPW], xao[DPW];
   bool xok[DPW];
+  float xg[DPW];   // xok as a 0 / 1 multiplier (ONE: the zero-padding multiply without a per-chunk select)
   auto tile_slots = [&](const Cur& q, unsigned (&o0)[DPW], unsigned (&o1)[DPW]) {
     const unsigned pbase = ((unsigned)q.n * d.H + q.h0) * d.W + q.w0;
 #pragma unroll
@@ -209,10 +230,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
     if (q.c == 0) tile_slots(q, ib0, ib1);
     const int ca = q.c + kc0;                       // the chunk's index in the whole reduction
     const int cn0 = ca * 16;
-    const bool s1sel = d.nsrc > 1 && cn0 >= C0;
+    const bool s1sel = !ONE && d.nsrc > 1 && cn0 >= C0;
     const int cl = s1sel ? cn0 - C0 : cn0;
     const int Cs = s1sel ? s1.C : C0;
-    const bool rag = cl + 16 > Cs;                  // the chunk's upper channel half is past the source
+    const bool rag = !ONE && cl + 16 > Cs;          // the chunk's upper channel half is past the source
     const rsrc4_t rs = s1sel ? rs1 : rs0;
     const unsigned img = l32 + (ACT ? Lay::OFF_RAW + q.s2 * Lay::IMG : Lay::OFF_COMP + q.s3 * Lay::IMG);
     if (!(ABL & 1) || prologue) {
@@ -269,7 +290,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
       for (int k = 0; k < DPW; ++k) {
         const int y = q.h0 + soy[k], x = q.w0 + sox[k];
         xok[k] = ((unsigned)y < (unsigned)d.H) & ((unsigned)x < (unsigned)d.W);
-        const bool in = xok[k] && (unsigned)soy[k] < (unsigned)TH && (unsigned)sox[k] < (unsigned)C5_W;
+        xg[k] = xok[k] ? 1.f : 0.f;
+        const bool in = xok[k] && (unsigned)soy[k] < (unsigned)TH && (unsigned)sox[k] < (unsigned)C5_W &&
+                        wave + k * NWV < NI;    // (dead slots: OOB here, so the store offset needs no select)
         const unsigned pix = pbase + (unsigned)(soy[k] * d.W + sox[k]);
         xao[k] = in ? (pix * (unsigned)C0 + 8u * hbit[k]) * 2u : OOB;
       }
@@ -277,10 +300,22 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
     const int cn0 = (q.c + kc0) * 16;
     // src0 (activation) or, for SK_ACT_PLAIN, src1 (stored: copied)
     const bool act = SK == SK_ACT || !(d.nsrc > 1 && cn0 >= C0);
-    const bool rag = cn0 + 16 > C0;
+    const bool rag = !ONE && cn0 + 16 > C0;
     const unsigned char* rb = raw_buf(q.s2);
     unsigned char* cb = comp_buf(q.s2);
     const float* tab = reinterpret_cast<const float*>(lds + Lay::OFF_TAB);
+    // this lane's 8 channels' scale / shift, read once per chunk (hbit is the same for all its slots; the
+    // compiler would re-read them per slot: the slot's LDS store may alias the table as far as it knows)
+    f2_t sc[4], sf[4];
+    if (act) {
+      const int ch = cn0 + 8 * hbit[0];             // < C0 + 8: the table is zero-padded there
+      const float4 a0 = *reinterpret_cast<const float4*>(tab + ch);
+      const float4 a1 = *reinterpret_cast<const float4*>(tab + ch + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_TABS + ch);
+      const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_TABS + ch + 4);
+      sc[0] = f2_t{a0.x, a0.y}; sc[1] = f2_t{a0.z, a0.w}; sc[2] = f2_t{a1.x, a1.y}; sc[3] = f2_t{a1.z, a1.w};
+      sf[0] = f2_t{b0.x, b0.y}; sf[1] = f2_t{b0.z, b0.w}; sf[2] = f2_t{b1.x, b1.y}; sf[3] = f2_t{b1.z, b1.w};
+    }
 #pragma unroll
     for (int k = 0; k < DPW; ++k) {
       const int i = wave + k * NWV;
@@ -289,18 +324,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
       const unsigned so = live ? (unsigned)s * 16u : (unsigned)(Lay::OFF_JUNK + lane * 16);
       uint4 q4 = *reinterpret_cast<const uint4*>((live ? rb : lds) + so);
       if (act) {
-        const int ch = cn0 + 8 * hbit[k];           // < C0 + 8: the table is zero-padded there
-        const bool ok = xok[k] && !(rag && hbit[k]);
-        const float4 a0 = *reinterpret_cast<const float4*>(tab + ch);
-        const float4 a1 = *reinterpret_cast<const float4*>(tab + ch + 4);
-        const float4 b0 = *reinterpret_cast<const float4*>(tab + C5_TABS + ch);
-        const float4 b1 = *reinterpret_cast<const float4*>(tab + C5_TABS + ch + 4);
-        const f2_t sc[4] = {{a0.x, a0.y}, {a0.z, a0.w}, {a1.x, a1.y}, {a1.z, a1.w}};
-        const f2_t sf[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
-        float gm = ok ? 1.f : 0.f;
+        const bool ok = xok[k] && !(rag && hbit[k]);   // ONE: rag is false
+        float gm = ONE ? xg[k] : (ok ? 1.f : 0.f);
         if constexpr (gated) {
+          // (a padding or dead slot's gate value is a zero load: sigmoid stays finite, times xg = 0)
           const float pv = *reinterpret_cast<const float*>(gate_buf(q.ti) + (live ? i : 0) * 256 + lane * 4);
-          gm = ok ? sigmoidf_(pv * ga + gb) : 0.f;
+          gm = ONE ? xg[k] * sigmoidf_(pv * ga + gb) : (ok ? sigmoidf_(pv * ga + gb) : 0.f);
         }
         const f2_t g2 = {gm, gm};
         float v[8];
@@ -319,7 +348,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
         // and dead slots and in the other blocks (zero-size resource), so every transform of an activation
         // chunk issues exactly DPW (ns_prev: the next chunk's wait leaves them in flight)
         if constexpr (OM == OM5_Y) {
-          const unsigned vo = (!live || (rag && hbit[k])) ? OOB : xao[k] + (unsigned)cn0 * 2u;
+          const unsigned vo = (ONE || !(rag && hbit[k])) ? xao[k] + (unsigned)cn0 * 2u : OOB;
           typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q4), rao, (int)vo, 0, 0);
         }
@@ -464,9 +493,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   // the next chunks' DMAs (their issue follows the epilogue)
   uint2 yv[OM == OM5_BNB ? MI : 1][NJ][4];
   const rsrc_t ry1 = mk_rsrc(OM == OM5_BNB ? d.bnb_y : d.out, (unsigned)(npix * d.Cout * 2));
-  auto load_y1 = [&](int ti) {
-    int n, h0, w0;
-    tile_of(ti, n, h0, w0);
+  auto load_y1 = [&](const Cur& q) {   // K's tile (its last chunk)
+    const int n = q.n, h0 = q.h0, w0 = q.w0;
     const int ow = w0 + (lane & 31), oh0 = h0 + wm * MI;
     const unsigned pix0 = ((unsigned)n * d.H + oh0) * (unsigned)d.W + ow;
 #pragma unroll
@@ -482,6 +510,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
         }
   };
   for (int ti = 0; ti < ntl; ++ti) {
+    const int tn = K.n, th0 = K.h0, tw0 = K.w0;     // this tile's origin (K is at its first chunk)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -494,7 +523,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
       // next chunk is readable by every wave)
       const bool last = c == nch - 1;
       if constexpr (OM == OM5_BNB) {
-        if (last) load_y1(ti);
+        if (last) load_y1(K);
       }
       if constexpr (PIPE) {
         load_col(K, 1, xB, wB);
@@ -533,8 +562,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
       if (sum == 12345.f) ((float*)d.out)[tid] = sum;
       continue;
     }
-    int n, h0, w0;
-    tile_of(ti, n, h0, w0);
+    const int n = tn, h0 = th0, w0 = tw0;
     const int pxl = lane & 31, hh = lane >> 5;
     const int ow = w0 + pxl;
     const bool colok = ow < d.W;
@@ -1017,10 +1045,11 @@ static int launch5_split(const unet_conv_desc* d, int S, hipStream_t st) {
 template <typename T, int OM>
 static int dispatch5_om(const unet_conv_desc* d, hipStream_t st) {
   const unet_src& s0 = d->src[0];
-  if (s0.kind != UNET_SRC_ACT) return launch5<T, OM, SK_PLAIN, 0>(d, st);
+  const bool one = d->nsrc == 1 && s0.C % 16 == 0;
+  if (s0.kind != UNET_SRC_ACT) return one ? launch5<T, OM, SK5_PLAIN1, 0>(d, st) : launch5<T, OM, SK_PLAIN, 0>(d, st);
   const bool g = s0.gate_p != nullptr;
   if constexpr (OM == OM5_Y) {
-    if (d->nsrc == 1) return g ? launch5<T, OM, SK_ACT, 1>(d, st) : launch5<T, OM, SK_ACT, 0>(d, st);
+    if (one) return g ? launch5<T, OM, SK_ACT, 1>(d, st) : launch5<T, OM, SK_ACT, 0>(d, st);
   }
   return g ? launch5<T, OM, SK_ACT_PLAIN, 1>(d, st) : launch5<T, OM, SK_ACT_PLAIN, 0>(d, st);
 }
@@ -1030,7 +1059,10 @@ static int dispatch5(const unet_conv_desc* d, hipStream_t st) {
   if (!conv5_eligible(d)) {
     const int S = conv5_splitk(d);
     const unet_src& s0 = d->src[0];
-    if (s0.kind != UNET_SRC_ACT) return launch5_split<T, SK_PLAIN, 0>(d, S, st);
+    const bool one = d->nsrc == 1 && s0.C % 16 == 0;
+    if (s0.kind != UNET_SRC_ACT)
+      return one ? launch5_split<T, SK5_PLAIN1, 0>(d, S, st) : launch5_split<T, SK_PLAIN, 0>(d, S, st);
+    if (one) return s0.gate_p ? launch5_split<T, SK_ACT, 1>(d, S, st) : launch5_split<T, SK_ACT, 0>(d, S, st);
     return s0.gate_p ? launch5_split<T, SK_ACT_PLAIN, 1>(d, S, st) : launch5_split<T, SK_ACT_PLAIN, 0>(d, S, st);
   }
   if (d->out_mode == UNET_OUT_F32) return dispatch5_om<T, OM5_F32>(d, st);
@@ -1067,5 +1099,6 @@ extern "C" int unet_diag_conv5_ablate(const unet_conv_desc* d, int abl, void* st
   using namespace unet;
   if (!conv5_eligible(d) || d->nsrc != 1 || d->out_mode != UNET_OUT_Y || d->dtype != UNET_BF16) return UNET_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  return d->src[0].kind == UNET_SRC_PLAIN ? abl5<SK_PLAIN, 0>(d, abl, st) : abl5<SK_ACT, 0>(d, abl, st);
+  if (d->src[0].C % 16) return UNET_ERR_ARG;
+  return d->src[0].kind == UNET_SRC_PLAIN ? abl5<SK5_PLAIN1, 0>(d, abl, st) : abl5<SK_ACT, 0>(d, abl, st);
 }

@@ -340,40 +340,43 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) { sc[j] = s.scale[cx + j]; sf[j] = s.shift[cx + j]; }
   }
-  uint4 qx[IX], qd[ID];
-  float gx[IX];
-  auto issue = [&](long long t) {
+  // two register sets of staged loads (tiles t+1 and t+2 in flight while tile t is computed from LDS): one tile
+  // in flight per block left the loop a memory round trip per 64-pixel tile (the 512^2 1x1 weight gradients ran
+  // at ~1.6 TB/s, profiles/r04_final_layerprof.txt)
+  uint4 qx[2][IX], qd[2][ID];
+  float gx[2][IX];
+  auto issue = [&](int b, long long t) {
     const long long pbase = t * PW_KP;
 #pragma unroll
     for (int k = 0; k < IX; ++k) {
       const int pr = (tid + 256 * k) / NVX;
       const long long p = pbase + pr;
-      const bool ok = pr < PW_KP && p < P && cx_ok;
-      qx[k] = pw_ld(xr, ok ? (unsigned)p * xpix + (unsigned)cx * 2u : PW_OOB, 0);
-      gx[k] = ok ? 1.f : 0.f;
-      if (ok && act && s.gate_p) gx[k] = sigmoidf_(s.gate_p[p] * s.gate_ab[0] + s.gate_ab[1]);
+      const bool ok = t < t_end && pr < PW_KP && p < P && cx_ok;
+      qx[b][k] = pw_ld(xr, ok ? (unsigned)p * xpix + (unsigned)cx * 2u : PW_OOB, 0);
+      gx[b][k] = ok ? 1.f : 0.f;
+      if (ok && act && s.gate_p) gx[b][k] = sigmoidf_(s.gate_p[p] * s.gate_ab[0] + s.gate_ab[1]);
     }
 #pragma unroll
     for (int k = 0; k < ID; ++k) {
       const int pr = (tid + 256 * k) / NVD;
       const long long p = pbase + pr;
-      const bool ok = pr < PW_KP && p < P && cd_ok;
-      qd[k] = pw_ld(dr, ok ? (unsigned)p * dpix + (unsigned)cd * 2u : PW_OOB, 0);
+      const bool ok = t < t_end && pr < PW_KP && p < P && cd_ok;
+      qd[b][k] = pw_ld(dr, ok ? (unsigned)p * dpix + (unsigned)cd * 2u : PW_OOB, 0);
     }
   };
-  auto finish = [&](T* buf) {
+  auto finish = [&](int b, T* buf) {
     T* bd = buf;
     T* bx = buf + PW_KP * RSD;
 #pragma unroll
     for (int k = 0; k < IX; ++k) {
       const int pr = (tid + 256 * k) / NVX;
       if (pr < PW_KP)
-        *reinterpret_cast<F*>(bx + pr * RSX + vx * 8) = pw_act<T>(qx[k], act, sc, sf, lo, gx[k]);
+        *reinterpret_cast<F*>(bx + pr * RSX + vx * 8) = pw_act<T>(qx[b][k], act, sc, sf, lo, gx[b][k]);
     }
 #pragma unroll
     for (int k = 0; k < ID; ++k) {
       const int pr = (tid + 256 * k) / NVD;
-      if (pr < PW_KP) *reinterpret_cast<uint4*>(bd + pr * RSD + vd * 8) = qd[k];
+      if (pr < PW_KP) *reinterpret_cast<uint4*>(bd + pr * RSD + vd * 8) = qd[b][k];
     }
   };
 
@@ -383,21 +386,12 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, 
 #pragma unroll
     for (int b = 0; b < MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (t_begin < t_end) {
-    issue(t_begin);
-    finish(lds);
-  }
-  __syncthreads();
   // tr-read lane geometry: group g reads pixel rows k0 + 8g + q (+4); odd groups take the +4 half first
   // (bank spread) — A and B apply the same K permutation, so the MFMA sums are unchanged
   const int g = lane >> 4, q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
   const int sw = (g & 1) * 4;
-  for (long long t = t_begin; t < t_end; ++t) {
-    const int cur = (int)((t - t_begin) & 1);
-    const T* bd = lds + cur * BUF;
+  auto compute = [&](const T* bd) {
     const T* bx = bd + PW_KP * RSD;
-    const bool has_next = t + 1 < t_end;
-    if (has_next) issue(t + 1);
 #pragma unroll
     for (int k0 = 0; k0 < PW_KP; k0 += 32) {
       const int r0 = k0 + 8 * g + q + sw, r1 = k0 + 8 * g + q + 4 - sw;
@@ -412,7 +406,24 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, 
         for (int a = 0; a < MA; ++a) acc[a][b] = Mma<T>::mma(av[a], bv, acc[a][b]);
       }
     }
-    if (has_next) finish(lds + (cur ^ 1) * BUF);
+  };
+
+  if (t_begin < t_end) {
+    issue(0, t_begin);
+    issue(1, t_begin + 1);
+    finish(0, lds);
+  }
+  __syncthreads();
+  // tile t sits in LDS buffer (t - t_begin) & 1; tiles past t_end load nothing (zero, never finished)
+  for (long long t = t_begin; t < t_end; t += 2) {
+    issue(0, t + 2);
+    compute(lds);
+    if (t + 1 < t_end) finish(1, lds + BUF);
+    __syncthreads();
+    if (t + 1 >= t_end) break;
+    issue(1, t + 3);
+    compute(lds + BUF);
+    if (t + 2 < t_end) finish(0, lds);
     __syncthreads();
   }
 
