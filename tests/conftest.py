@@ -45,3 +45,14 @@ def golden_modules():
 @pytest.fixture(scope="session")
 def golden_losses():
     return load_golden("losses.pt")
+
+
+@pytest.fixture(autouse=True)
+def _guard_check_after_test():
+    """UNET_GUARD=1 runs (bounds-checking debug mode, csrc/guard_alloc.cpp): after each test, check the guard bands
+    of every live device allocation once more — this also covers the torch ops that ran after the test's last
+    HIP-library call (the library checks around its own calls)."""
+    yield
+    if os.environ.get("UNET_GUARD", "") not in ("", "0"):
+        from unet._hip import lib as L
+        L.guard_check("end of test (torch ops after the last library call)")
