@@ -19,9 +19,6 @@
 
 namespace unet {
 
-#ifndef PW_PREFETCH
-#define PW_PREFETCH 0   // 1: the next wave tile's first loads issued before this tile's epilogue (more VGPRs)
-#endif
 constexpr unsigned PW_OOB = 0x40000000u;  // >= every tensor byte size admitted below (< 1 GiB)
 typedef __amdgpu_buffer_rsrc_t pw_rsrc_t;
 
@@ -56,7 +53,7 @@ __device__ __forceinline__ typename Mma<T>::frag pw_act(uint4 q, bool act, const
 // gate_bwd1: d(x*s) and s = sigmoid(psi) are loaded ahead of the MFMAs).  Distinct instantiations also keep
 // the forward and the dgrads apart in kernel traces and PMC passes (tools/traffic.py)
 template <typename T, int NA, int NB, int OMK>
-__global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, long long P, int nchunks) {
+__global__ __launch_bounds__(256, 2) void pw_conv_kernel(const unet_conv_desc d, long long P, int nchunks) {
   constexpr bool GATED = OMK == 2;
   typedef typename Mma<T>::frag F;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -76,26 +73,42 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
   const long long tstride = (long long)gridDim.x * 4;
   long long tile = (long long)blockIdx.x * 4 + wave;
 
-  // this lane's pixels (one per px tile) and their gate multipliers; pixels past P read as 0 (OOB) and
-  // are forced to 0 after the transform
+  // this lane's pixels (one per px tile) and their gate pre-activations; pixels past P read as 0 (OOB) and
+  // are forced to 0 after the transform.  Every (tile, chunk) step's operands — the x vectors, the weight
+  // fragments and the BN scale / shift of the chunk — are loaded one step ahead, across tile boundaries too
+  // (round 5: the weights and scale / shift were loaded by the step that used them, and a tile's first x
+  // chunk at its start: ~3 memory round trips per 64-pixel tile, 5.8 us per tile per wave at 512^2)
+  const bool gate = act && s.gate_p != nullptr;
   unsigned xoff[NB];
-  float gm[NB];
-  uint4 xq[NB];
-  auto setup = [&](long long t) {
+  float gp[NB], gok[NB], gm[NB];
+  auto setup = [&](long long t, uint4 (&xv)[NB]) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const long long p = t * (16 * NB) + 16 * b + i16;
       const bool ok = t < ntiles && p < P;
       xoff[b] = ok ? (unsigned)p * pixb + (unsigned)g * 16u : PW_OOB;
-      gm[b] = ok ? 1.f : 0.f;
-      if (ok && act && s.gate_p) gm[b] = sigmoidf_(s.gate_p[p] * s.gate_ab[0] + s.gate_ab[1]);
+      gok[b] = ok ? 1.f : 0.f;
+      gp[b] = (ok && gate) ? s.gate_p[p] : 0.f;
     }
 #pragma unroll
-    for (int b = 0; b < NB; ++b) xq[b] = pw_ld(xr, xoff[b], 0);
+    for (int b = 0; b < NB; ++b) xv[b] = pw_ld(xr, xoff[b], 0);
   };
-#if PW_PREFETCH
-  setup(tile);
-#endif
+  auto stage = [&](int c, uint4 (&wv)[NA], float4 (&scv)[2], float4 (&sfv)[2]) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      wv[a] = pw_ld(wr, (unsigned)lane * 16u, ((unsigned)(co0 / 16 + a) * nchunks + c) * 1024u);
+    if (act) {
+      const int ch = c * 32 + g * 8;
+      scv[0] = *reinterpret_cast<const float4*>(s.scale + ch);
+      scv[1] = *reinterpret_cast<const float4*>(s.scale + ch + 4);
+      sfv[0] = *reinterpret_cast<const float4*>(s.shift + ch);
+      sfv[1] = *reinterpret_cast<const float4*>(s.shift + ch + 4);
+    }
+  };
+  uint4 xq[NB], wq[NA];
+  float4 scq[2], sfq[2];
+  setup(tile, xq);
+  stage(0, wq, scq, sfq);
 
   float sm[NA][4], sq[NA][4];   // OMK 0: BN partial sums over all of this wave's tiles (pixels past P add 0)
 #pragma unroll
@@ -105,9 +118,8 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
 
   for (; tile < ntiles; tile += tstride) {
     const long long pw0 = tile * (16 * NB);
-#if !PW_PREFETCH
-    setup(tile);
-#endif
+#pragma unroll
+    for (int b = 0; b < NB; ++b) gm[b] = gate ? gok[b] * sigmoidf_(gp[b] * s.gate_ab[0] + s.gate_ab[1]) : gok[b];
     f32x4 acc[NA][NB];
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -151,43 +163,34 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(const unet_conv_desc d, lo
       }
     }
     for (int c = 0; c < nchunks; ++c) {
-      uint4 xn[NB];
-      if (c + 1 < nchunks) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) xn[b] = pw_ld(xr, xoff[b], (unsigned)(c + 1) * 64u);
-      }
-      uint4 wq[NA];
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-        wq[a] = pw_ld(wr, (unsigned)lane * 16u, ((unsigned)(co0 / 16 + a) * nchunks + c) * 1024u);
-      float sc[8], sf[8];
-      if (act) {
-        const int ch = c * 32 + g * 8;
-        const float4 s0 = *reinterpret_cast<const float4*>(s.scale + ch);
-        const float4 s1 = *reinterpret_cast<const float4*>(s.scale + ch + 4);
-        const float4 f0 = *reinterpret_cast<const float4*>(s.shift + ch);
-        const float4 f1 = *reinterpret_cast<const float4*>(s.shift + ch + 4);
-        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-        sf[0] = f0.x; sf[1] = f0.y; sf[2] = f0.z; sf[3] = f0.w; sf[4] = f1.x; sf[5] = f1.y; sf[6] = f1.z; sf[7] = f1.w;
-      }
+      const float sc[8] = {scq[0].x, scq[0].y, scq[0].z, scq[0].w, scq[1].x, scq[1].y, scq[1].z, scq[1].w};
+      const float sf[8] = {sfq[0].x, sfq[0].y, sfq[0].z, sfq[0].w, sfq[1].x, sfq[1].y, sfq[1].z, sfq[1].w};
       F xb[NB];
 #pragma unroll
       for (int b = 0; b < NB; ++b) xb[b] = pw_act<T>(xq[b], act, sc, sf, lo, gm[b]);
+      // the next step's operands (the next chunk, or the next tile's first chunk)
+      uint4 xn[NB], wn[NA];
+      float4 scn[2], sfn[2];
+      if (c + 1 < nchunks) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) xn[b] = pw_ld(xr, xoff[b], (unsigned)(c + 1) * 64u);
+        stage(c + 1, wn, scn, sfn);
+      } else {
+        setup(tile + tstride, xn);
+        stage(0, wn, scn, sfn);
+      }
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
         const F wa = __builtin_bit_cast(F, wq[a]);
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[a][b] = Mma<T>::mma(wa, xb[b], acc[a][b]);
       }
-      if (c + 1 < nchunks) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) xq[b] = xn[b];
-      }
+      for (int b = 0; b < NB; ++b) xq[b] = xn[b];
+#pragma unroll
+      for (int a = 0; a < NA; ++a) wq[a] = wn[a];
+      scq[0] = scn[0]; scq[1] = scn[1]; sfq[0] = sfn[0]; sfq[1] = sfn[1];
     }
-#if PW_PREFETCH
-    // the next tile's pixels and first chunk, in flight during this tile's epilogue
-    setup(tile + tstride);
-#endif
 
     // epilogue: acc[a][b][r] = out[px = pw0 + 16b + i16][co = co0 + 16a + 4g + r]
     if constexpr (OMK == 0) {
@@ -305,7 +308,7 @@ __device__ __forceinline__ typename Mma<T>::frag pw_tr8(const T* r0, const T* r1
 }
 
 template <typename T, int MA, int MB>
-__global__ __launch_bounds__(256) void pw_wgrad_kernel(const unet_wgrad_desc d, long long P, int per_split, float* ws) {
+__global__ __launch_bounds__(256, 2) void pw_wgrad_kernel(const unet_wgrad_desc d, long long P, int per_split, float* ws) {
   typedef typename Mma<T>::frag F;
   constexpr int BCO = 16 * MA, BCI = 64 * MB;
   // LDS row strides: odd multiples of 32 B (see wgrad2.hip) so the tr reads are conflict-free
@@ -560,9 +563,11 @@ bool pw_conv_ok(const unet_conv_desc* d) {
   return (double)P * d->Cin * 2 < (double)PW_OOB;
 }
 
+// NA = 4 (64 output channels per wave) with 32-pixel wave tiles: the 64-pixel ones needed 268-292 registers, one
+// wave per SIMD (round 5); every instantiation is bounded to 256 (two waves per SIMD, __launch_bounds__(256, 2))
 static void pw_conv_geom(const unet_conv_desc* d, int& na, int& nb) {
   na = d->Cout % 64 == 0 ? 4 : (d->Cout % 32 == 0 ? 2 : 1);
-  nb = 4;
+  nb = na == 4 ? 2 : 4;
 }
 
 // blocks along the pixels: the pw_conv_kernel waves are persistent over wave tiles (16 NB pixels each); up to
@@ -602,7 +607,7 @@ template <typename T>
 static int pw_conv_t(const unet_conv_desc* d, hipStream_t st) {
   int na, nb;
   pw_conv_geom(d, na, nb);
-  if (na == 4) return launch_pw<T, 4, 4>(d, st);
+  if (na == 4) return launch_pw<T, 4, 2>(d, st);
   if (na == 2) return launch_pw<T, 2, 4>(d, st);
   return launch_pw<T, 1, 4>(d, st);
 }
@@ -636,7 +641,7 @@ bool pw_wgrad_ok(const unet_wgrad_desc* d) {
 static PwWPlan pw_wplan(const unet_wgrad_desc* d) {
   PwWPlan p{};
   p.ma = d->Cout % 64 == 0 ? 4 : (d->Cout % 32 == 0 ? 2 : 1);
-  p.mb = d->Cin % 256 == 0 ? 4 : (d->Cin % 128 == 0 ? 2 : 1);
+  p.mb = d->Cin % 128 == 0 ? 2 : 1;   // (MB = 4 needed 320-413 registers: one wave per SIMD or spills)
   const long long P = (long long)d->N * d->H * d->W;
   const long long ntiles = (P + PW_KP - 1) / PW_KP;
   const long long blocks_out = (long long)(d->Cout / (16 * p.ma)) * (d->Cin / (64 * p.mb));
@@ -668,9 +673,9 @@ static int launch_pww(const unet_wgrad_desc* d, const PwWPlan& p, hipStream_t st
 int pw_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
   const PwWPlan p = pw_wplan(d);
   int e;
-  if (p.ma == 4) e = p.mb == 4 ? launch_pww<4, 4>(d, p, st) : p.mb == 2 ? launch_pww<4, 2>(d, p, st) : launch_pww<4, 1>(d, p, st);
-  else if (p.ma == 2) e = p.mb == 4 ? launch_pww<2, 4>(d, p, st) : p.mb == 2 ? launch_pww<2, 2>(d, p, st) : launch_pww<2, 1>(d, p, st);
-  else e = p.mb == 4 ? launch_pww<1, 4>(d, p, st) : p.mb == 2 ? launch_pww<1, 2>(d, p, st) : launch_pww<1, 1>(d, p, st);
+  if (p.ma == 4) e = p.mb == 2 ? launch_pww<4, 2>(d, p, st) : launch_pww<4, 1>(d, p, st);
+  else if (p.ma == 2) e = p.mb == 2 ? launch_pww<2, 2>(d, p, st) : launch_pww<2, 1>(d, p, st);
+  else e = p.mb == 2 ? launch_pww<1, 2>(d, p, st) : launch_pww<1, 1>(d, p, st);
   if (e) return e;
   // slabs -> PW_RG partial slabs (written after the split slabs in the workspace) -> dw
   const long long total = (long long)d->Cout * d->Cin;
