@@ -939,7 +939,8 @@ bool conv5_eligible(const unet_conv_desc* d) {
 // the real epilogue (y + BN partial sums, y + BN-backward sums, or fp32 with split / accumulation).
 // UNET_CONV5_SPLIT=0 turns it off (A/B).
 int conv5_splitk(const unet_conv_desc* d) {
-  static const int on = [] { const char* e = getenv("UNET_CONV5_SPLIT"); return e ? atoi(e) : 1; }();
+  const char* e = getenv("UNET_CONV5_SPLIT");   // read per call (tests flip it)
+  const int on = e ? atoi(e) : 1;
   if (!on || conv5_mode() == 0 || d->act_out || !conv5_shape_ok(d)) return 1;
   if (d->Cout > 1024 || (d->Cout & (d->Cout - 1))) return 1;     // the finisher's channel-vector layout
   const long long work = conv5_mtiles(d) * cdiv(d->Cout, C5_BN);
