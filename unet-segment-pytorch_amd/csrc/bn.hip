@@ -53,6 +53,16 @@ __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long lon
                                    float eps, float* mean, float* invstd, float* scale, float* shift) {
   __shared__ double sh2[32];
   const int c = blockIdx.x;
+  // the per-channel operands of the epilogue, loaded before the partial rows (in flight together: the kernel is
+  // a chain of dependent memory round trips, and these need not be one of them)
+  float g_ = 0.f, b_ = 0.f, rm_ = 0.f, rv_ = 0.f;
+  long long nb_ = 0;
+  if (threadIdx.x == 0) {
+    g_ = gamma[c];
+    b_ = beta[c];
+    if (rmean && rvar) { rm_ = rmean[c]; rv_ = rvar[c]; }
+    if (nbt && momentum < 0) nb_ = *nbt;
+  }
   double s = 0, ss = 0;
   const float* s0 = stats + (size_t)c * rows;         // [2][C][rows]: contiguous over r
   const float* s1 = stats + ((size_t)C + c) * rows;
@@ -78,15 +88,15 @@ __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long lon
     const double is = 1.0 / sqrt(var + (double)eps);
     mean[c] = (float)m;
     invstd[c] = (float)is;
-    const float sc = (float)((double)gamma[c] * is);
+    const float sc = (float)((double)g_ * is);
     scale[c] = sc;
-    shift[c] = (float)((double)beta[c] - m * (double)gamma[c] * is);
+    shift[c] = (float)((double)b_ - m * (double)g_ * is);
     if (rmean && rvar) {
       double f = momentum;
-      if (momentum < 0) f = nbt ? 1.0 / (double)(*nbt + 1) : 1.0;  // momentum=None: cumulative average
+      if (momentum < 0) f = nbt ? 1.0 / (double)(nb_ + 1) : 1.0;  // momentum=None: cumulative average
       const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
-      rmean[c] = (float)((1.0 - f) * (double)rmean[c] + f * m);
-      rvar[c] = (float)((1.0 - f) * (double)rvar[c] + f * unb);
+      rmean[c] = (float)((1.0 - f) * (double)rm_ + f * m);
+      rvar[c] = (float)((1.0 - f) * (double)rv_ + f * unb);
     }
     if (c == 0 && nbt) *nbt += 1;
   }
@@ -388,6 +398,19 @@ __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, 
                                        float* dbeta, int accum, float* coef) {
   __shared__ double sh2[32];
   const int c = blockIdx.x;
+  // the epilogue's per-channel operands, in flight with the partial rows (as bn_finalize_kernel)
+  float g_ = 0.f, is_ = 0.f, mu_ = 0.f, dg_ = 0.f, db_ = 0.f;
+  if (threadIdx.x == 0) {
+    if (coef) {
+      g_ = gamma[c];
+      is_ = invstd[c];
+      if (count > 0) mu_ = mean[c];
+    }
+    if (accum) {
+      if (dgamma) dg_ = dgamma[c];
+      if (dbeta) db_ = dbeta[c];
+    }
+  }
   double a = 0, b = 0;
   const int B = blockDim.x;
   int r = threadIdx.x;
@@ -405,16 +428,16 @@ __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, 
   }
   block_sum2_d(a, b, sh2);
   if (threadIdx.x == 0) {
-    if (dbeta) dbeta[c] = accum ? dbeta[c] + (float)a : (float)a;
-    if (dgamma) dgamma[c] = accum ? dgamma[c] + (float)b : (float)b;
+    if (dbeta) dbeta[c] = accum ? db_ + (float)a : (float)a;
+    if (dgamma) dgamma[c] = accum ? dg_ + (float)b : (float)b;
     if (coef) {
-      const double k = (double)gamma[c] * invstd[c];
+      const double k = (double)g_ * is_;
       coef[c] = (float)k;
       if (count > 0) {
         const double M = (double)count;
-        const double B = -k * (double)invstd[c] * b / M;
+        const double B = -k * (double)is_ * b / M;
         coef[C + c] = (float)B;
-        coef[2 * C + c] = (float)(-k * a / M - B * (double)mean[c]);
+        coef[2 * C + c] = (float)(-k * a / M - B * (double)mu_);
       } else {
         coef[C + c] = 0.f;
         coef[2 * C + c] = 0.f;

@@ -985,17 +985,18 @@ int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
   return 0;
 }
 
-// PIPE: the column-ahead operand reads for the y and fp32 epilogues (per layer 5-9 % faster: 117 -> 108 us on
-// the 512^2 64->64 forward, profiles/r04_layerprof_conv5_pipe{0,1}.txt); the BN-backward-sums epilogue keeps
-// the compiler's schedule: with both operand columns and its 16 y1 registers live it ran out of VGPRs
-// (256 + 108 bytes of scratch) and went 14-30 % slower
+// PIPE: the column-ahead operand reads (per layer 5-9 % faster: 117 -> 108 us on the 512^2 64->64 forward,
+// profiles/r04_layerprof_conv5_pipe{0,1}.txt).  The BN-backward-sums epilogue of a stored source (the dgrads'
+// dy) has it too since round 5's register cuts (245-251 VGPRs, no spills); with a BN-activation source
+// (SK_ACT_PLAIN) both operand columns plus its 32 y1 registers still run out of VGPRs (256 + 28-36 bytes of
+// scratch), so that form keeps the compiler's schedule (round 4: 14-30 % slower with the spills)
 // The 8-wave form (NWV 8).  The one-wave-per-SIMD form (NWV 4: 64 channels per wave, 12 LDS reads per 24 MFMAs
 // per tap column, 462-502 registers, no spills) measured 10-25 % slower on every layer
 // (profiles/r04_layerprof_conv5_{8,4}waves.txt): one wave cannot cover its own LDS and DMA latencies.
-template <typename T, int OM, int SK, int GATE, int ABL = 0>
+template <typename T, int OM, int SK, int GATE, int ABL = 0, int PIPE_ = -1>
 static int launch5(const unet_conv_desc* d, hipStream_t st) {
   constexpr int TH = C5_WM * C5_MI;
-  constexpr int PIPE = OM == OM5_BNB ? 0 : 1;
+  constexpr int PIPE = PIPE_ >= 0 ? PIPE_ : (OM == OM5_BNB && SK != SK_PLAIN && SK != SK5_PLAIN1) ? 0 : 1;
   const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH);
   const int mt = d->N * tw * th;
   const int gy = cdiv(d->Cout, C5_BN);
@@ -1047,6 +1048,10 @@ template <typename T, int OM>
 static int dispatch5_om(const unet_conv_desc* d, hipStream_t st) {
   const unet_src& s0 = d->src[0];
   const bool one = d->nsrc == 1 && s0.C % 16 == 0;
+  if constexpr (OM == OM5_BNB) {   // UNET_C5_BNB_PIPE=0: the round-4 schedule of the dy dgrads (A/B)
+    const char* e = getenv("UNET_C5_BNB_PIPE");
+    if (one && s0.kind != UNET_SRC_ACT && e && !atoi(e)) return launch5<T, OM, SK5_PLAIN1, 0, 0, 0>(d, st);
+  }
   if (s0.kind != UNET_SRC_ACT) return one ? launch5<T, OM, SK5_PLAIN1, 0>(d, st) : launch5<T, OM, SK_PLAIN, 0>(d, st);
   const bool g = s0.gate_p != nullptr;
   if constexpr (OM == OM5_Y) {
