@@ -1,6 +1,8 @@
 """Ablation timing of conv5_kernel (csrc/conv5.hip, bf16 y mode) on full-size layers (diagnostic, GPU).
 Modes (bits): 1 no in-loop halo DMA; 2 no in-loop weight DMA; 4 no epilogue stores / sums; 8 no per-chunk
-barrier; 16 no BN transform.  Times are medians of 10 launches; results are garbage for modes != 0."""
+barrier; 16 no BN transform.  Times are medians of 10 launches; results are garbage for modes != 0.
+--split: the split-K form on the small maps (the split kernel alone with the same bits; mode -1 = its y + BN-stats
+finisher alone)."""
 import ctypes
 import os
 os.environ["UNET_CONV5"] = "1"
@@ -19,7 +21,11 @@ lib = L.load()
 lib.unet_diag_conv5_ablate.argtypes = [ctypes.POINTER(L.ConvDesc), ctypes.c_int, ctypes.c_void_p]
 if "--conv5" in sys.argv:     # accepted for older command lines
     sys.argv.remove("--conv5")
-FN = lib.unet_diag_conv5_ablate
+lib.unet_diag_conv5_split_ablate.argtypes = [ctypes.POINTER(L.ConvDesc), ctypes.c_int, ctypes.c_void_p]
+SPLIT = "--split" in sys.argv
+if SPLIT:
+    sys.argv.remove("--split")
+FN = lib.unet_diag_conv5_split_ablate if SPLIT else lib.unet_diag_conv5_ablate
 
 
 def layer(N, H, W, cin, cout, kind):
@@ -43,13 +49,18 @@ def layer(N, H, W, cin, cout, kind):
     rows = lib.unet_conv_stats_rows(d)
     st = f32(2, cout, rows, device=dev)
     d.stats = st.data_ptr()
-    return d, (x, w, wp, ab, y, st)
+    ws = torch.empty(max(lib.unet_conv_workspace(ctypes.byref(d)), 16), dtype=torch.uint8, device=dev)
+    d.workspace = ws.data_ptr()
+    return d, (x, w, wp, ab, y, st, ws)
 
 
 def main():
     modes = [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,3,4,8,7,15,16,31").split(",")]
-    for (N, H, W, cin, cout, kind) in [(4, 512, 512, 64, 64, L.SRC_ACT), (4, 512, 512, 64, 64, L.SRC_PLAIN),
-                                       (4, 256, 256, 128, 128, L.SRC_ACT), (4, 128, 128, 256, 256, L.SRC_PLAIN)]:
+    layers = [(4, 512, 512, 64, 64, L.SRC_ACT), (4, 512, 512, 64, 64, L.SRC_PLAIN),
+              (4, 256, 256, 128, 128, L.SRC_ACT), (4, 128, 128, 256, 256, L.SRC_PLAIN)]
+    if SPLIT:
+        layers = [(4, 32, 32, 512, 512, L.SRC_ACT), (4, 32, 32, 512, 512, L.SRC_PLAIN), (4, 64, 64, 512, 256, L.SRC_ACT)]
+    for (N, H, W, cin, cout, kind) in layers:
         d, keep = layer(N, H, W, cin, cout, kind)
         fl = 2.0 * N * H * W * cin * cout * 9
         stream = torch.cuda.current_stream().cuda_stream

@@ -782,9 +782,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
 // sums of the stored gradient (bnb_stats[2][rows][Cout], conv5's OM5_BNB); 2: fp32, split across out / out2,
 // optionally accumulating
 // ------------------------------------------------------------------------------------------------
-template <typename T, int MODE>
+constexpr int FIN_TRIPS = 8;   // pixels per lane of a finisher block (fin_rows)
+template <typename T, int MODE, int S>
 __global__ __launch_bounds__(256) void conv5_splitk_finish_kernel(const unet_conv_desc d, const float* __restrict__ ws,
-                                                                  int S, int rows) {
+                                                                  int rows) {
   __shared__ float4 red[2][256];
   const int CV = d.Cout >> 2, R = 256 / CV, tid = threadIdx.x;
   const int cv = tid % CV, r = tid / CV, co = cv * 4;
@@ -800,44 +801,68 @@ __global__ __launch_bounds__(256) void conv5_splitk_finish_kernel(const unet_con
       sf = *reinterpret_cast<const float4*>(d.bnb_shift + co);
     }
   }
-  for (long long p = p0 + r; p < p1; p += R) {
-    const float4* src = reinterpret_cast<const float4*>(ws + (size_t)p * d.Cout + co);
-    float4 v = src[0];
-    for (int z = 1; z < S; ++z) {
-      const float4 q = src[(size_t)z * (slab / 4)];
-      v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
-    }
-    if constexpr (MODE == 0 || MODE == 1) {
-      uint2 pk;
-      pk.x = pack2_16<T>(v.x, v.y);
-      pk.y = pack2_16<T>(v.z, v.w);
-      *reinterpret_cast<uint2*>((T*)d.out + (size_t)p * d.Cout + co) = pk;
-      if constexpr (MODE == 0) {
-        sa.x += v.x; sa.y += v.y; sa.z += v.z; sa.w += v.w;
-        sb.x = __builtin_fmaf(v.x, v.x, sb.x); sb.y = __builtin_fmaf(v.y, v.y, sb.y);
-        sb.z = __builtin_fmaf(v.z, v.z, sb.z); sb.w = __builtin_fmaf(v.w, v.w, sb.w);
-      } else {
-        float g[4], y[4];
-        unpack4_16<T>(pk, g);
-        unpack4_16<T>(*reinterpret_cast<const uint2*>((const T*)d.bnb_y + (size_t)p * d.Cout + co), y);
-        const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, sfv[4] = {sf.x, sf.y, sf.z, sf.w};
-        float gg[4];
+  // FIN_TRIPS pixels per lane at once: every slab load (and the BNB y1 loads) of a lane issued before the first
+  // add — one memory round trip per batch instead of one per pixel (the loop was latency-bound: 10-17 us for a
+  // 4 x 32^2 x 512 finish, profiles/r05_conv5_split_ablate.txt).  Per element the slabs still add in slab order
+  // and each lane's BN sums in pixel order: the same results as one pixel at a time.
+  constexpr int U = FIN_TRIPS;
+  for (long long pb = p0 + r; pb < p1; pb += (long long)R * U) {
+    float4 v[U];
+    uint2 yb[U];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) gg[k] = (d.bnb_relu && !(y[k] * scv[k] + sfv[k] > 0.f)) ? 0.f : g[k];
-        sa.x += gg[0]; sa.y += gg[1]; sa.z += gg[2]; sa.w += gg[3];
-        sb.x = __builtin_fmaf(gg[0], y[0], sb.x); sb.y = __builtin_fmaf(gg[1], y[1], sb.y);
-        sb.z = __builtin_fmaf(gg[2], y[2], sb.z); sb.w = __builtin_fmaf(gg[3], y[3], sb.w);
+    for (int u = 0; u < U; ++u) {
+      const long long p = pb + (long long)u * R;
+      const long long pc = p < p1 ? p : p1 - 1;     // clamped: loads unconditional, results unused past p1
+      v[u] = *reinterpret_cast<const float4*>(ws + (size_t)pc * d.Cout + co);
+      if constexpr (MODE == 1) yb[u] = *reinterpret_cast<const uint2*>((const T*)d.bnb_y + (size_t)pc * d.Cout + co);
+    }
+#pragma unroll
+    for (int z = 1; z < S; ++z)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long p = pb + (long long)u * R;
+        const long long pc = p < p1 ? p : p1 - 1;
+        const float4 q = *reinterpret_cast<const float4*>(ws + (size_t)z * slab + (size_t)pc * d.Cout + co);
+        v[u].x += q.x; v[u].y += q.y; v[u].z += q.z; v[u].w += q.w;
       }
-    } else {
-      float4* o;
-      int acc;
-      if (co < d.split) { o = reinterpret_cast<float4*>((float*)d.out + (size_t)p * d.split + co); acc = d.accum; }
-      else { o = reinterpret_cast<float4*>((float*)d.out2 + (size_t)p * (d.Cout - d.split) + (co - d.split)); acc = d.accum2; }
-      if (acc) {
-        const float4 b = *o;
-        v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long p = pb + (long long)u * R;
+      if (p >= p1) break;
+      const float4 vv = v[u];
+      if constexpr (MODE == 0 || MODE == 1) {
+        uint2 pk;
+        pk.x = pack2_16<T>(vv.x, vv.y);
+        pk.y = pack2_16<T>(vv.z, vv.w);
+        *reinterpret_cast<uint2*>((T*)d.out + (size_t)p * d.Cout + co) = pk;
+        if constexpr (MODE == 0) {
+          sa.x += vv.x; sa.y += vv.y; sa.z += vv.z; sa.w += vv.w;
+          sb.x = __builtin_fmaf(vv.x, vv.x, sb.x); sb.y = __builtin_fmaf(vv.y, vv.y, sb.y);
+          sb.z = __builtin_fmaf(vv.z, vv.z, sb.z); sb.w = __builtin_fmaf(vv.w, vv.w, sb.w);
+        } else {
+          float g[4], y[4];
+          unpack4_16<T>(pk, g);
+          unpack4_16<T>(yb[u], y);
+          const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, sfv[4] = {sf.x, sf.y, sf.z, sf.w};
+          float gg[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) gg[k] = (d.bnb_relu && !(y[k] * scv[k] + sfv[k] > 0.f)) ? 0.f : g[k];
+          sa.x += gg[0]; sa.y += gg[1]; sa.z += gg[2]; sa.w += gg[3];
+          sb.x = __builtin_fmaf(gg[0], y[0], sb.x); sb.y = __builtin_fmaf(gg[1], y[1], sb.y);
+          sb.z = __builtin_fmaf(gg[2], y[2], sb.z); sb.w = __builtin_fmaf(gg[3], y[3], sb.w);
+        }
+      } else {
+        float4* o;
+        int acc;
+        if (co < d.split) { o = reinterpret_cast<float4*>((float*)d.out + (size_t)p * d.split + co); acc = d.accum; }
+        else { o = reinterpret_cast<float4*>((float*)d.out2 + (size_t)p * (d.Cout - d.split) + (co - d.split)); acc = d.accum2; }
+        float4 w = vv;
+        if (acc) {
+          const float4 b2 = *o;
+          w.x += b2.x; w.y += b2.y; w.z += b2.z; w.w += b2.w;
+        }
+        *o = w;
       }
-      *o = v;
     }
   }
   if constexpr (MODE == 0 || MODE == 1) {
@@ -959,7 +984,6 @@ size_t conv5_workspace(const unet_conv_desc* d) {
 }
 
 // the finisher: 256 threads = CV channel vectors (4 channels) x R pixel lanes, FIN_TRIPS pixels per lane
-constexpr int FIN_TRIPS = 8;
 static int fin_rows(const unet_conv_desc* d) {
   const int R = 256 / (d->Cout / 4);
   const long long npix = (long long)d->N * d->H * d->W;
@@ -1007,6 +1031,23 @@ static int launch5(const unet_conv_desc* d, hipStream_t st) {
   return check_launch("conv5");
 }
 
+template <typename T, int MODE>
+static void launch5_finish_m(const unet_conv_desc* d, int S, hipStream_t st) {
+  const int rows = fin_rows(d);
+  const float* ws = (const float*)d->workspace;
+  if (S == 2) hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, MODE, 2>), dim3(rows), dim3(256), 0, st, *d, ws, rows);
+  else if (S == 4) hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, MODE, 4>), dim3(rows), dim3(256), 0, st, *d, ws, rows);
+  else hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, MODE, 8>), dim3(rows), dim3(256), 0, st, *d, ws, rows);
+}
+// the finisher of a split-K conv (S in {2, 4, 8}: conv5_splitk)
+template <typename T>
+static int launch5_finish(const unet_conv_desc* d, int S, hipStream_t st) {
+  if (d->out_mode == UNET_OUT_F32) launch5_finish_m<T, 2>(d, S, st);
+  else if (d->bnb_stats) launch5_finish_m<T, 1>(d, S, st);
+  else launch5_finish_m<T, 0>(d, S, st);
+  return check_launch("conv5 split finish");
+}
+
 // split-K: the conv into S fp32 slabs (one workgroup per tile and split), then the finisher
 template <typename T, int SK, int GATE>
 static int launch5_split(const unet_conv_desc* d, int S, hipStream_t st) {
@@ -1031,15 +1072,7 @@ static int launch5_split(const unet_conv_desc* d, int S, hipStream_t st) {
   hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM5_F32, SK, GATE, 0, 1, 8, true>), dim3(mt, gy, S), dim3(512), 0, st, k,
                      tw, th, mt, nch / S, nch);
   if (int e = check_launch("conv5 split")) return e;
-  const int rows = fin_rows(d);
-  const float* ws = (const float*)d->workspace;
-  if (d->out_mode == UNET_OUT_F32)
-    hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, 2>), dim3(rows), dim3(256), 0, st, *d, ws, S, rows);
-  else if (d->bnb_stats)
-    hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, 1>), dim3(rows), dim3(256), 0, st, *d, ws, S, rows);
-  else
-    hipLaunchKernelGGL((conv5_splitk_finish_kernel<T, 0>), dim3(rows), dim3(256), 0, st, *d, ws, S, rows);
-  return check_launch("conv5 split finish");
+  return launch5_finish<T>(d, S, st);
 }
 
 // source kind of a descriptor: plain, one BN activation (gated or not), or a BN activation + a stored map.
@@ -1097,7 +1130,55 @@ static int abl5(const unet_conv_desc* d, int abl, hipStream_t st) {
   return UNET_ERR_ARG;
 }
 
+// split-K ablations: the split kernel alone (ABL bits as above) or, abl < 0, the y + BN-stats finisher alone
+template <int SK>
+static int abl5_split(const unet_conv_desc* d, int abl, hipStream_t st) {
+  constexpr int TH = C5_WM * C5_MI;
+  const int S = conv5_splitk(d);
+  const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH), mt = d->N * tw * th, gy = cdiv(d->Cout, C5_BN);
+  const int nch = cdiv(d->Cin, 16);
+  if (S < 2 || !d->workspace) return UNET_ERR_ARG;
+  if (abl < 0) {
+    launch5_finish_m<bf16, 0>(d, S, st);
+    return check_launch("conv5 split finish (diag)");
+  }
+  unet_conv_desc k = *d;
+  k.out_mode = UNET_OUT_F32;
+  k.out = d->workspace;
+  k.out2 = nullptr;
+  k.split = d->Cout;
+  k.accum = k.accum2 = 0;
+  k.stats = nullptr;
+  k.bnb_stats = nullptr;
+  k.act_out = nullptr;
+  const dim3 grid(mt, gy, S);
+#define C5SA(A) hipLaunchKernelGGL((conv5_kernel<bf16, C5_MI, OM5_F32, SK, 0, A, 1, 8, true>), grid, dim3(512), 0, st, k, tw, th, mt, nch / S, nch)
+  switch (abl) {
+    case 0: C5SA(0); break;
+    case 1: C5SA(1); break;
+    case 2: C5SA(2); break;
+    case 3: C5SA(3); break;
+    case 4: C5SA(4); break;
+    case 8: C5SA(8); break;
+    case 16: C5SA(16); break;
+    case 31: C5SA(31); break;
+    default: return UNET_ERR_ARG;
+  }
+#undef C5SA
+  return check_launch("conv5 split (diag)");
+}
+
 }  // namespace unet
+
+// diagnostic (not part of the C ABI header): the split-K form's ablations (abl5_split) on a one-source plain or
+// BN-activation bf16 y-mode descriptor whose map is small enough for split-K (d->workspace set); tools/conv5_ablate.py
+extern "C" int unet_diag_conv5_split_ablate(const unet_conv_desc* d, int abl, void* stream) {
+  using namespace unet;
+  if (conv5_eligible(d) || d->nsrc != 1 || d->out_mode != UNET_OUT_Y || d->dtype != UNET_BF16 || d->src[0].C % 16)
+    return UNET_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return d->src[0].kind == UNET_SRC_PLAIN ? abl5_split<SK5_PLAIN1>(d, abl, st) : abl5_split<SK_ACT>(d, abl, st);
+}
 
 // diagnostic (not part of the C ABI header): conv5 ablations of the bf16 y-mode kernel (ABL bits above) on a
 // one-source plain or BN-activation descriptor; tools/conv5_ablate.py

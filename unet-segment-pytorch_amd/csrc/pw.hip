@@ -307,7 +307,7 @@ __device__ __forceinline__ typename Mma<T>::frag pw_tr8(const T* r0, const T* r1
   return __builtin_bit_cast(typename Mma<T>::frag, r);
 }
 
-template <typename T, int MA, int MB>
+template <typename T, int MA, int MB, bool GATED>
 __global__ __launch_bounds__(256, 2) void pw_wgrad_kernel(const unet_wgrad_desc d, long long P, int per_split, float* ws) {
   typedef typename Mma<T>::frag F;
   constexpr int BCO = 16 * MA, BCI = 64 * MB;
@@ -331,6 +331,9 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_kernel(const unet_wgrad_desc 
   const unsigned xpix = (unsigned)d.Cin * 2u, dpix = (unsigned)d.Cout * 2u;
   const pw_rsrc_t xr = pw_rsrc(s.data, (unsigned)(P * xpix));
   const pw_rsrc_t dr = pw_rsrc(d.dy, (unsigned)(P * dpix));
+  const pw_rsrc_t gr_ = pw_rsrc(GATED ? (const void*)s.gate_p : s.data, (unsigned)(GATED ? P * 4 : 0));
+  float ga = 0.f, gb = 0.f;
+  if (GATED) { ga = s.gate_ab[0]; gb = s.gate_ab[1]; }
 
   // fixed per-thread channel vectors (NVX, NVD divide 256)
   const int vx = tid % NVX, vd = tid % NVD;
@@ -343,11 +346,13 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_kernel(const unet_wgrad_desc 
 #pragma unroll
     for (int j = 0; j < 8; ++j) { sc[j] = s.scale[cx + j]; sf[j] = s.shift[cx + j]; }
   }
-  // two register sets of staged loads (tiles t+1 and t+2 in flight while tile t is computed from LDS): one tile
-  // in flight per block left the loop a memory round trip per 64-pixel tile (the 512^2 1x1 weight gradients ran
-  // at ~1.6 TB/s, profiles/r04_final_layerprof.txt)
-  uint4 qx[2][IX], qd[2][ID];
-  float gx[2][IX];
+  // NQ register sets of staged loads: tiles t+1 .. t+NQ in flight while tile t is computed from LDS.  The loop
+  // is a memory round trip per NQ tiles: with 2 sets the 512^2 1x1 weight gradients ran at ~1.7 TB/s (round 5,
+  // profiles/r05_*), i.e. latency-bound; the gate pre-activation is loaded with the tile and turned into its
+  // sigmoid when the tile is written to LDS (a sigmoid at issue time waited for its load right there)
+  constexpr int NQ = 4;
+  uint4 qx[NQ][IX], qd[NQ][ID];
+  float gv[NQ][IX], gp[NQ][IX];
   auto issue = [&](int b, long long t) {
     const long long pbase = t * PW_KP;
 #pragma unroll
@@ -356,8 +361,9 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_kernel(const unet_wgrad_desc 
       const long long p = pbase + pr;
       const bool ok = t < t_end && pr < PW_KP && p < P && cx_ok;
       qx[b][k] = pw_ld(xr, ok ? (unsigned)p * xpix + (unsigned)cx * 2u : PW_OOB, 0);
-      gx[b][k] = ok ? 1.f : 0.f;
-      if (ok && act && s.gate_p) gx[b][k] = sigmoidf_(s.gate_p[p] * s.gate_ab[0] + s.gate_ab[1]);
+      gv[b][k] = ok ? 1.f : 0.f;
+      if constexpr (GATED)
+        gp[b][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr_, ok ? (int)((unsigned)p * 4u) : (int)PW_OOB, 0, 0));
     }
 #pragma unroll
     for (int k = 0; k < ID; ++k) {
@@ -373,8 +379,9 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_kernel(const unet_wgrad_desc 
 #pragma unroll
     for (int k = 0; k < IX; ++k) {
       const int pr = (tid + 256 * k) / NVX;
-      if (pr < PW_KP)
-        *reinterpret_cast<F*>(bx + pr * RSX + vx * 8) = pw_act<T>(qx[b][k], act, sc, sf, lo, gx[b][k]);
+      float gm = gv[b][k];
+      if constexpr (GATED) gm = gm * sigmoidf_(gp[b][k] * ga + gb);
+      if (pr < PW_KP) *reinterpret_cast<F*>(bx + pr * RSX + vx * 8) = pw_act<T>(qx[b][k], act, sc, sf, lo, gm);
     }
 #pragma unroll
     for (int k = 0; k < ID; ++k) {
@@ -412,22 +419,23 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_kernel(const unet_wgrad_desc 
   };
 
   if (t_begin < t_end) {
-    issue(0, t_begin);
-    issue(1, t_begin + 1);
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) issue(b, t_begin + b);
     finish(0, lds);
   }
   __syncthreads();
-  // tile t sits in LDS buffer (t - t_begin) & 1; tiles past t_end load nothing (zero, never finished)
-  for (long long t = t_begin; t < t_end; t += 2) {
-    issue(0, t + 2);
-    compute(lds);
-    if (t + 1 < t_end) finish(1, lds + BUF);
-    __syncthreads();
-    if (t + 1 >= t_end) break;
-    issue(1, t + 3);
-    compute(lds + BUF);
-    if (t + 2 < t_end) finish(0, lds);
-    __syncthreads();
+  // tile t: register set (t - t_begin) % NQ, LDS buffer (t - t_begin) & 1; a set is re-issued (tile t + NQ) as
+  // soon as its tile is in LDS; tiles past t_end load nothing (zeros, never finished)
+  for (long long t = t_begin; t < t_end; t += NQ) {
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const long long tj = t + j;
+      if (tj >= t_end) break;
+      issue(j, tj + NQ);
+      compute(lds + (j & 1) * BUF);
+      if (tj + 1 < t_end) finish((j + 1) % NQ, lds + ((j + 1) & 1) * BUF);
+      __syncthreads();
+    }
   }
 
   // slab ws[split][co][ci]; C layout: row (co) = 4*(l>>4)+r, col (ci) = l&15
@@ -646,7 +654,12 @@ static PwWPlan pw_wplan(const unet_wgrad_desc* d) {
   const long long ntiles = (P + PW_KP - 1) / PW_KP;
   const long long blocks_out = (long long)(d->Cout / (16 * p.ma)) * (d->Cin / (64 * p.mb));
   const size_t slab = (size_t)d->Cout * d->Cin * sizeof(float);
-  long long s = (1024 + blocks_out - 1) / blocks_out;            // ~1024 workgroups
+  // workgroup target: one or two per CU.  Each split writes (and the reduction reads back) a whole fp32 slab of
+  // the weight gradient, so more splits cost slab traffic: with 4 tiles in flight per workgroup, 256 - 512
+  // workgroups measured 10-26 % faster than the former 1024 (tools/pww_ab.py, profiles/r05_pww_blocks.txt)
+  const char* e = getenv("UNET_PWW_BLOCKS");   // A/B of the workgroup target (read per call)
+  const long long target = e && atoll(e) > 0 ? atoll(e) : (slab >= (16u << 10) ? 256 : 512);
+  long long s = (target + blocks_out - 1) / blocks_out;
   const long long cap = (long long)(((size_t)64 << 20) / slab);  // slab traffic <= 64 MB
   if (s > cap) s = cap;
   if (s > ntiles) s = ntiles;
@@ -663,10 +676,15 @@ template <int MA, int MB>
 static int launch_pww(const unet_wgrad_desc* d, const PwWPlan& p, hipStream_t st) {
   const long long P = (long long)d->N * d->H * d->W;
   dim3 grid(p.splits, d->Cin / (64 * MB), d->Cout / (16 * MA));
-  if (d->dtype == UNET_F16)
-    hipLaunchKernelGGL((pw_wgrad_kernel<f16, MA, MB>), grid, dim3(256), 0, st, *d, P, p.per_split, (float*)d->workspace);
-  else
-    hipLaunchKernelGGL((pw_wgrad_kernel<bf16, MA, MB>), grid, dim3(256), 0, st, *d, P, p.per_split, (float*)d->workspace);
+  const bool g = d->src[0].kind == UNET_SRC_ACT && d->src[0].gate_p;
+  float* ws = (float*)d->workspace;
+  if (d->dtype == UNET_F16) {
+    if (g) hipLaunchKernelGGL((pw_wgrad_kernel<f16, MA, MB, true>), grid, dim3(256), 0, st, *d, P, p.per_split, ws);
+    else hipLaunchKernelGGL((pw_wgrad_kernel<f16, MA, MB, false>), grid, dim3(256), 0, st, *d, P, p.per_split, ws);
+  } else {
+    if (g) hipLaunchKernelGGL((pw_wgrad_kernel<bf16, MA, MB, true>), grid, dim3(256), 0, st, *d, P, p.per_split, ws);
+    else hipLaunchKernelGGL((pw_wgrad_kernel<bf16, MA, MB, false>), grid, dim3(256), 0, st, *d, P, p.per_split, ws);
+  }
   return check_launch("pw_wgrad");
 }
 
