@@ -1,4 +1,5 @@
-"""Op test of `unet_materialize` (csrc/misc.hip, the packed-fp32 per-element kernel since round 4): the
+"""Op test of `unet_materialize` (csrc/misc.hip: the LDS-tiled Up-block kernel since round 5 for 16-bit maps, the
+packed-fp32 per-element kernel otherwise and under UNET_MAT_TILE=0): the
 bilinear x2 upsample (align_corners=True) of relu?(y * scale + shift), placed with the skip-size padding —
 the decoder input of every Up block (reference unet/models/layers.py:78,183 `nn.Upsample(scale_factor=2,
 mode='bilinear', align_corners=True)` + the pad of :98-102) — against F.interpolate / F.pad in fp64.
@@ -94,3 +95,34 @@ def test_materialize_vs_fp64_interpolate(shape, prec, relu):
     print(f"\n{prec} relu={int(relu)} {shape}: max|err| {float(err.max()):.3e}, max err/tol {float((err / tol).max()):.3f}, "
           f"fraction within half an output ulp of the exact value {half:.6f}")
     assert not bool(bad.any()), (int(bad.sum()), float((err / tol).max()))
+
+
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("shape", SHAPES + [(1, 9, 7, 8, 23, 20), (3, 11, 40, 16, 22, 85), (2, 8, 8, 24, 16, 16)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_materialize_tile_bit_identical_to_per_pixel(shape, prec, relu, monkeypatch):
+    """The tiled form (materialize_up_tile_kernel) stages the source span once and blends from LDS with the same
+    tap indices, weights and fma order as the per-pixel form: the two maps are bit-identical (C = 8 / 16 / 24:
+    one and two channel vectors per block, and a channel count the tiled form leaves to the per-pixel one)."""
+    from unet._hip import lib as L
+    from unet._hip import runtime as R
+    N, h, w, C, H, W = shape
+    pad_t, pad_l = (H - 2 * h) // 2, (W - 2 * w) // 2
+    torch.manual_seed(29)
+    y = torch.randn(N, h, w, C, device="cuda").to(DT[prec])
+    ab = torch.stack([torch.randn(C, device="cuda"), torch.randn(C, device="cuda") * 0.2])
+    s = L.Src()
+    s.kind, s.H, s.W, s.C, s.data = L.SRC_UP_ACT, h, w, C, y.data_ptr()
+    s.scale, s.shift, s.relu = ab[0].data_ptr(), ab[1].data_ptr(), int(relu)
+    s.up_h, s.up_w, s.pad_t, s.pad_l = 2 * h, 2 * w, pad_t, pad_l
+    s.sh, s.sw = R.up_scale(h, 2 * h), R.up_scale(w, 2 * w)
+    outs = []
+    for tile in ("1", "0"):
+        monkeypatch.setenv("UNET_MAT_TILE", tile)
+        o = torch.full((N, H, W, C), float("nan"), dtype=DT[prec], device="cuda")
+        L.call("unet_materialize", R._PRECISIONS[prec].code, s, N, H, W, o.data_ptr(), R.stream())
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert not outs[0].isnan().any()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))

@@ -856,6 +856,103 @@ __global__ void materialize_fast_kernel(const MatDesc d, long long N, int H, int
   }
 }
 
+// The Up block's decoder input (layers.py:98-102: bilinear x2 upsample, align_corners=True, of relu(BN(x1)), then
+// F.pad to x2's size) as LDS tiles (round 5).  The per-pixel form above gathers the 4 bilinear taps of every output
+// vector from L2 and runs the BN affine on each (4 x the reads and the affine work of the source it needs); here a
+// block owns MUP_TJ output rows x MUP_TX output columns x MUP_CT channel vectors, stages the source rows / columns
+// they touch once (<= MUP_TJ/2+2 x MUP_TX/2+2 for scales <= 1/2, host-checked) as fp32 activations in LDS, and
+// blends each output from there — with the same tap indices, weights and fma order as item_issue / item_finish
+// (mode 4), so the map is bit-identical to the per-pixel form and to the convs' virtual UP_ACT sources.
+constexpr int MUP_TJ = 8, MUP_TX = 32, MUP_SJ = MUP_TJ / 2 + 2, MUP_SX = MUP_TX / 2 + 2, MUP_CT = 8;
+template <typename T>
+__global__ __launch_bounds__(256) void materialize_up_tile_kernel(const unet_src s, int H, int W, T* out) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  __shared__ float4 tile[MUP_SJ * MUP_SX * MUP_CT * 2];   // 8 fp32 activations (2 float4) per source vector
+  const int C = s.C, CV = C >> 3;
+  const int CT = CV < MUP_CT ? CV : MUP_CT;               // a power of two: a thread keeps one channel vector
+  const int tid = threadIdx.x, cv = tid & (CT - 1);
+  const int tiles_h = (H + MUP_TJ - 1) / MUP_TJ;
+  const int n = (int)blockIdx.y / tiles_h, oy0 = ((int)blockIdx.y - n * tiles_h) * MUP_TJ;
+  const int ox0 = (int)blockIdx.x * MUP_TX;
+  const int c = ((int)blockIdx.z * CT + cv) * 8;          // this thread's first channel
+  // the up-region rows / columns the tile covers and the source span they read
+  int ua = oy0 - s.pad_t, ub = oy0 + MUP_TJ - 1 - s.pad_t, va = ox0 - s.pad_l, vb = ox0 + MUP_TX - 1 - s.pad_l;
+  ua = ua < 0 ? 0 : ua; ub = ub > s.up_h - 1 ? s.up_h - 1 : ub;
+  va = va < 0 ? 0 : va; vb = vb > s.up_w - 1 ? s.up_w - 1 : vb;
+  int sy0 = 0, sx0 = 0, ny = 0, nx = 0;
+  if (ua <= ub && va <= vb) {
+    int i0, i1;
+    float l;
+    lin_idx(s.sh, ua, s.H, i0, i1, l);
+    sy0 = i0;
+    lin_idx(s.sh, ub, s.H, i0, i1, l);
+    ny = i1 - sy0 + 1;
+    lin_idx(s.sw, va, s.W, i0, i1, l);
+    sx0 = i0;
+    lin_idx(s.sw, vb, s.W, i0, i1, l);
+    nx = i1 - sx0 + 1;
+    ny = ny < MUP_SJ ? ny : MUP_SJ;                        // (host-checked; a clamp keeps LDS in bounds regardless)
+    nx = nx < MUP_SX ? nx : MUP_SX;
+  }
+  float sc[8], sf[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = s.scale[c + j]; sf[j] = s.shift[c + j]; }
+  // phase 1: the source span -> LDS, BN affine (+ ReLU) in fp32 as item_finish applies it per tap
+  const T* src = (const T*)s.data;
+  for (int i = tid; i < ny * nx * CT; i += 256) {
+    const int px = i / CT, sxr = px % nx, syr = px / nx;
+    const unsigned pix = ((unsigned)n * s.H + (unsigned)(sy0 + syr)) * (unsigned)s.W + (unsigned)(sx0 + sxr);
+    float t[8];
+    unpack16<T>(*reinterpret_cast<const uint4*>(src + (size_t)pix * C + c), t);
+    float a[8];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      f2 r = __builtin_elementwise_fma(f2{t[j], t[j + 1]}, f2{sc[j], sc[j + 1]}, f2{sf[j], sf[j + 1]});
+      if (s.relu) r = f2{fmaxf(r[0], 0.f), fmaxf(r[1], 0.f)};
+      a[j] = r[0];
+      a[j + 1] = r[1];
+    }
+    float4* d4 = tile + ((syr * MUP_SX + sxr) * MUP_CT + cv) * 2;
+    d4[0] = make_float4(a[0], a[1], a[2], a[3]);
+    d4[1] = make_float4(a[4], a[5], a[6], a[7]);
+  }
+  __syncthreads();
+  // phase 2: the outputs (zero outside the up region: F.pad)
+  for (int i = tid; i < MUP_TJ * MUP_TX * CT; i += 256) {
+    const int px = i / CT, oxr = px % MUP_TX, oyr = px / MUP_TX;
+    const int oy = oy0 + oyr, ox = ox0 + oxr;
+    if (oy >= H || ox >= W) continue;
+    const int uy = oy - s.pad_t, ux = ox - s.pad_l;
+    float v[8];
+    if (uy >= 0 && uy < s.up_h && ux >= 0 && ux < s.up_w) {
+      int y0, y1, x0, x1;
+      float ly, lx;
+      lin_idx(s.sh, uy, s.H, y0, y1, ly);
+      lin_idx(s.sw, ux, s.W, x0, x1, lx);
+      const float hy0 = 1.f - ly, wx0 = 1.f - lx;
+      const float w0s = hy0 * wx0, w1s = hy0 * lx, w2s = ly * wx0, w3s = ly * lx;
+      const f2 w0 = {w0s, w0s}, w1 = {w1s, w1s}, w2 = {w2s, w2s}, w3 = {w3s, w3s};
+      const float4* r0 = tile + (((y0 - sy0) * MUP_SX + (x0 - sx0)) * MUP_CT + cv) * 2;
+      const float4* r1 = tile + (((y0 - sy0) * MUP_SX + (x1 - sx0)) * MUP_CT + cv) * 2;
+      const float4* r2 = tile + (((y1 - sy0) * MUP_SX + (x0 - sx0)) * MUP_CT + cv) * 2;
+      const float4* r3 = tile + (((y1 - sy0) * MUP_SX + (x1 - sx0)) * MUP_CT + cv) * 2;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 a0 = r0[h], a1 = r1[h], a2 = r2[h], a3 = r3[h];
+        const f2 p0 = __builtin_elementwise_fma(w3, f2{a3.x, a3.y}, __builtin_elementwise_fma(w2, f2{a2.x, a2.y},
+                        __builtin_elementwise_fma(w1, f2{a1.x, a1.y}, w0 * f2{a0.x, a0.y})));
+        const f2 p1 = __builtin_elementwise_fma(w3, f2{a3.z, a3.w}, __builtin_elementwise_fma(w2, f2{a2.z, a2.w},
+                        __builtin_elementwise_fma(w1, f2{a1.z, a1.w}, w0 * f2{a0.z, a0.w})));
+        v[4 * h] = p0[0]; v[4 * h + 1] = p0[1]; v[4 * h + 2] = p1[0]; v[4 * h + 3] = p1[1];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    }
+    store_vec<T>(out + ((size_t)((unsigned)n * H + oy) * W + ox) * C + c, v);
+  }
+}
+
 // MaxPool2d(2) of relu?(scale*y + shift) with argmax codes; one thread per pooled channel vector
 // (I as materialize_fast_kernel)
 template <typename T, typename I = unsigned>
@@ -1149,6 +1246,25 @@ int unet_materialize(int dtype, const unet_src* src, long long N, int H, int W, 
   }
   const int vec = dtype != UNET_F32 ? 8 : 4;
   const long long total = N * H * (long long)W * ((src->C + vec - 1) / vec);
+  {
+    // the tiled Up-block form: 16-bit, C/8 a power of two, both scales <= 1/2 (the span bound of its LDS tile);
+    // UNET_MAT_TILE=0: the per-pixel form (A/B), read per call
+    const char* e = getenv("UNET_MAT_TILE");
+    const int cv8 = src->C / 8;
+    if ((!e || atoi(e)) && dtype != UNET_F32 && src->kind == UNET_SRC_UP_ACT && src->C % 8 == 0 && (cv8 & (cv8 - 1)) == 0 &&
+        src->scale && src->shift && src->sh <= 0.5f && src->sw <= 0.5f && src->sh >= 0.f && src->sw >= 0.f &&
+        N * H <= (1LL << 30) && (double)N * H * W * src->C < 4294967296.0 &&
+        (double)N * src->H * src->W * src->C < 4294967296.0) {
+      const int ct = cv8 < MUP_CT ? cv8 : MUP_CT;
+      const dim3 grid((unsigned)cdiv(W, MUP_TX), (unsigned)(N * cdiv(H, MUP_TJ)), (unsigned)(cv8 / ct));
+      hipStream_t st = (hipStream_t)stream;
+      if (dtype == UNET_BF16)
+        hipLaunchKernelGGL(materialize_up_tile_kernel<bf16>, grid, dim3(256), 0, st, *src, H, W, (bf16*)out);
+      else
+        hipLaunchKernelGGL(materialize_up_tile_kernel<f16>, grid, dim3(256), 0, st, *src, H, W, (f16*)out);
+      return check_launch("materialize up tile");
+    }
+  }
   long long b = (total + 255) / 256;
   const long long bcap = block_cap("UNET_MAT_BLOCKS", 4096);
   if (b > bcap) b = bcap;
