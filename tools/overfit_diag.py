@@ -154,6 +154,14 @@ class Hip:
         return {k: v.detach().double() for k, v in self.m.state_dict().items() if v.is_floating_point()}
 
 
+def _progress(what, e, epochs):
+    """a line every 25 epochs on the process's real stderr (past pytest's capture): long runs (the 200-epoch
+    protocol is minutes per execution) keep writing, so a runner that watches for silence does not take
+    them for hung"""
+    if e % 25 == 0 or e == epochs:
+        print(f"[overfit] {what}: epoch {e}/{epochs}", file=sys.__stderr__, flush=True)
+
+
 def run_oracle(init, names, x, t, epochs, dtype, snap=()):
     """Per-epoch (loss, Tumor-Dice); with `snap`, also the oracle's full state (parameters + BN buffers, as
     fp32 CPU tensors keyed like the state_dict) after each of those epochs (1-based)."""
@@ -161,6 +169,7 @@ def run_oracle(init, names, x, t, epochs, dtype, snap=()):
     hist, snaps = [], {}
     for e in range(1, epochs + 1):
         hist.append(o.epoch())
+        _progress(f"oracle {str(dtype).replace('torch.', '')}", e, epochs)
         if e in snap:
             snaps[e] = {k: (v.detach().float().cpu().clone() if v.is_floating_point() else v.cpu().clone())
                         for k, v in o.p.items()}
@@ -169,7 +178,11 @@ def run_oracle(init, names, x, t, epochs, dtype, snap=()):
 
 def run_hip(init, x, t, epochs, base, prec="fp32"):
     h = Hip(init, x, t, base, prec)
-    return [h.epoch() for _ in range(epochs)]
+    hist = []
+    for e in range(1, epochs + 1):
+        hist.append(h.epoch())
+        _progress(f"HIP {prec}", e, epochs)
+    return hist
 
 
 def _dist(a, b, keys):
