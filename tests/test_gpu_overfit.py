@@ -25,6 +25,7 @@ reference's own measured spread:
   * test_overfit_c1_full_protocol_final_dice: 200 epochs; the last-epoch Tumor-Dice within
     max(1e-3, max_k |ref32_k - ref64|) of the fp64 oracle's, the bound measured in the same test."""
 
+import contextlib
 import sys
 from pathlib import Path
 
@@ -75,12 +76,16 @@ def test_overfit_c1_tumor_dice_vs_reference_spread(c1):
 
 
 @pytest.fixture(scope="module")
-def c1_full(c1):
+def c1_full(c1, request):
     D, init, names, x, t = c1
-    hip = D.run_hip(init, x, t, 200, 64)
-    r32, snaps = D.run_oracle(init, names, x, t, 200, torch.float32, snap=set(PINS))
-    r32p = [D.run_oracle(D.perturb(init, names, s), names, x, t, 200, torch.float32) for s in (1, 2)]
-    r64 = D.run_oracle(init, names, x, t, 200, torch.float64)
+    # five 200-epoch executions (minutes): with pytest's output capture suspended, so their progress lines
+    # (tools/overfit_diag.py) reach the runner's log while they run
+    cm = request.config.pluginmanager.getplugin("capturemanager")
+    with cm.global_and_fixture_disabled() if cm is not None else contextlib.nullcontext():
+        hip = D.run_hip(init, x, t, 200, 64)
+        r32, snaps = D.run_oracle(init, names, x, t, 200, torch.float32, snap=set(PINS))
+        r32p = [D.run_oracle(D.perturb(init, names, s), names, x, t, 200, torch.float32) for s in (1, 2)]
+        r64 = D.run_oracle(init, names, x, t, 200, torch.float64)
     return hip, [r32] + r32p, r64, snaps
 
 
