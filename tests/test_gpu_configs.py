@@ -53,9 +53,10 @@ def _assert_16bit_paths(log, prec):
     assert any(n.startswith(f"conv5_kernel<{prec},") and m == 0 for n, m in log), sorted(names)
     assert any(n.startswith((f"conv5_kernel<{prec},", f"conv3_kernel<{prec},3,")) and m == 1 for n, m in log), \
         sorted(names)
-    # the small-map y outputs (down4 at 32^2, up1.conv.3 at 64^2): conv5's split-K form since round 5 (conv3 before)
-    assert any((n.startswith(f"conv5_kernel<{prec},") and "+splitk" in n or n.startswith(f"conv3_kernel<{prec},3,"))
-               and m == 0 for n, m in log), sorted(names)
+    # the small-map y outputs (down4 at 32^2, up1.conv.3 at 64^2): conv5's small-map forms since round 5 (split-K
+    # and / or the 8-row MI = 2 tiles; conv3 before)
+    assert any((n.startswith(f"conv5_kernel<{prec},") and ("+splitk" in n or n.startswith(f"conv5_kernel<{prec},2>"))
+                or n.startswith(f"conv3_kernel<{prec},3,")) and m == 0 for n, m in log), sorted(names)
     return names
 
 

@@ -140,16 +140,26 @@ def test_conv5_matches_conv3(prec, path, monkeypatch):
     assert rel <= 1e-5, rel
 
 
-# ---- split-K (round 5): maps whose 16 x 32 x 64 tiles do not fill the chip (down4 at 32^2, up1.conv.3 at 64^2) ----
+# ---- small maps (round 5): maps whose 16 x 32 x 64 tiles do not fill the chip (down4 at 32^2, up1.conv.3 at 64^2):
+# split-K over the input channels, and the 8-row (MI = 2) tiles, which halve the splits or need none.
+# mi2 "0": the MI = 4 split-K form alone (UNET_CONV5_MI2=0); "1": the default (MI = 2, split where still needed)
 SPLIT_SHAPES = [(4, 32, 32, 512, 512), (4, 64, 64, 512, 256), (2, 16, 16, 256, 128), (2, 16, 24, 64, 64)]
 
 
+def _small_map_form(v, prec, mi2):
+    if mi2 == "0":
+        return v.startswith(f"conv5_kernel<{TN[prec]},4>+splitk")
+    return v.startswith(f"conv5_kernel<{TN[prec]},2>")
+
+
+@pytest.mark.parametrize("mi2", ["0", "1"])
 @pytest.mark.parametrize("shape", SPLIT_SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("src", ["plain", "act", "act_gate", "concat"])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv5_splitk_y_stats(prec, src, shape):
-    """The split-K form against torch fp32 on the same operands: y and the BN partial sums (same gates as the
-    persistent form), and bit-identical across two runs (the slabs are added in a fixed order)."""
+def test_conv5_splitk_y_stats(prec, src, shape, mi2, monkeypatch):
+    """The small-map forms against torch fp32 on the same operands: y and the BN partial sums (same gates as the
+    persistent form), and bit-identical across two runs (split-K slabs are added in a fixed order)."""
+    monkeypatch.setenv("UNET_CONV5_MI2", mi2)
     L, R = _lib(), _rt()
     N, H, W, cin, cout = shape
     dt = DT[prec]
@@ -193,7 +203,7 @@ def test_conv5_splitk_y_stats(prec, src, shape):
         d = _conv(prec, srcs, N, H, W, cin, w, 3, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
         outs.append((out, st))
     v = _variant(d)
-    assert v.startswith(f"conv5_kernel<{TN[prec]},4>+splitk"), v
+    assert _small_map_form(v, prec, mi2), v
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])   # deterministic
     out, st = outs[0]
     ref = F.conv2d(x.permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
@@ -208,10 +218,12 @@ def test_conv5_splitk_y_stats(prec, src, shape):
 SPLIT_DGRAD_SHAPES = [(4, 32, 32, 512, 512), (4, 32, 32, 256, 512), (2, 16, 16, 256, 128), (2, 16, 24, 64, 64)]
 
 
+@pytest.mark.parametrize("mi2", ["0", "1"])
 @pytest.mark.parametrize("shape", SPLIT_DGRAD_SHAPES, ids=lambda s: "x".join(map(str, s)))
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_conv5_splitk_dgrad_f32_split_accum(prec, shape):
-    """The split-K fp32 dgrad epilogue: split across the concat, the first part accumulated, and unsplit."""
+def test_conv5_splitk_dgrad_f32_split_accum(prec, shape, mi2, monkeypatch):
+    """The small-map fp32 dgrad epilogues: split across the concat, the first part accumulated, and unsplit."""
+    monkeypatch.setenv("UNET_CONV5_MI2", mi2)
     L = _lib()
     N, H, W, cin, cout = shape
     dt = DT[prec]
@@ -227,7 +239,7 @@ def test_conv5_splitk_dgrad_f32_split_accum(prec, shape):
     d = _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
               split=split, accum=1, accum2=0)
     v = _variant(d)
-    assert "+splitk" in v, v
+    assert _small_map_form(v, prec, mi2), v
     _close_bf16(torch.cat([o1 - 0.5, o2], -1), ref, "dgrad f32")
     o = torch.full((N, H, W, cin), float("nan"), device="cuda")
     _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o.data_ptr(), split=cin)

@@ -479,12 +479,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   auto pin_col = [&]() {
     if constexpr (PIPE) {
       constexpr int NDS = MI + 2 + 3 * NJ, NMF = 3 * MI * NJ;   // reads of the next column, MFMAs of this one
+      constexpr int NP = NDS < NMF ? NDS : NMF;
 #pragma unroll
-      for (int i = 0; i < NDS; ++i) {
+      for (int i = 0; i < NP; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, NMF - NDS, 0);
+      if constexpr (NMF > NP) __builtin_amdgcn_sched_group_barrier(0x008, NMF - NP, 0);
+      if constexpr (NDS > NP) __builtin_amdgcn_sched_group_barrier(0x100, NDS - NP, 0);   // (MI = 2: 7 reads, 6 MFMAs)
     }
   };
   if constexpr (PIPE) load_col(K, 0, xA, wA);
@@ -899,7 +901,8 @@ __global__ __launch_bounds__(256) void conv5_splitk_finish_kernel(const unet_con
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-constexpr int C5_MI = 4;
+constexpr int C5_MI = 4;      // wave-tile rows of the large maps (16-row workgroup tiles)
+constexpr int C5_MI_S = 2;    // and of the small ones (8-row tiles: twice the tiles, round 5)
 
 // UNET_CONV5: unset = the measured default (below), 0 = never (conv3 everywhere), 1 = every eligible conv
 // (tests, ablations); read per call so tests can flip it
@@ -908,12 +911,22 @@ static int conv5_mode() {
   return e ? (atoi(e) ? 1 : 0) : 2;
 }
 
-static long long conv5_mtiles(const unet_conv_desc* d) {
-  return (long long)d->N * cdiv(d->W, C5_W) * cdiv(d->H, C5_WM * C5_MI);
+static long long conv5_mtiles(const unet_conv_desc* d, int mi) {
+  return (long long)d->N * cdiv(d->W, C5_W) * cdiv(d->H, C5_WM * mi);
 }
 
-static int conv5_gx(const unet_conv_desc* d) {
-  const long long mt = conv5_mtiles(d);
+// MI of a descriptor: 4 where its 16 x 32 x 64 tiles fill the chip (>= 256 workgroups), else 2 — 8 x 32 x 64
+// tiles, twice as many (the 64^2 layers then need no split-K, the 32^2 ones half the splits).  The 2-row wave
+// tile reads 7 LDS fragments per 6 MFMAs per tap column instead of 9 per 12 (LDS-bound nearer the MFMA peak)
+// but drops the split slabs' HBM round trip and the finisher.  UNET_CONV5_MI2=0: MI = 4 everywhere (A/B).
+static int conv5_mi(const unet_conv_desc* d) {
+  const char* e = getenv("UNET_CONV5_MI2");   // read per call
+  if (e && !atoi(e)) return C5_MI;
+  return conv5_mtiles(d, C5_MI) * cdiv(d->Cout, C5_BN) >= 256 ? C5_MI : C5_MI_S;
+}
+
+static int conv5_gx(const unet_conv_desc* d, int mi) {
+  const long long mt = conv5_mtiles(d, mi);
   const int gy = cdiv(d->Cout, C5_BN);
   long long gx = cdiv(256, gy);                     // one 8-wave workgroup per CU (LDS), persistent
   if (gx > mt) gx = mt;
@@ -951,9 +964,11 @@ bool conv5_eligible(const unet_conv_desc* d) {
   // default: every 16-bit y output (forward and the middle-activation dgrads) and the fp32 dgrads of <= 64
   // channels — per layer conv5 measured 0-31 % faster there (the 512^2 64-channel layers 14-31 %); the
   // wider fp32 dgrads stay on conv3, whose tiles measured 5-20 % faster (profiles/r03_layerprof_*.txt)
-  if (mode == 2 && d->out_mode == UNET_OUT_F32 && d->Cout > C5_BN) return false;
+  // (the small maps' MI = 2 form serves the wide fp32 dgrads too: conv3 there is a 64- or 128-workgroup launch)
   if (!conv5_shape_ok(d)) return false;
-  const long long work = conv5_mtiles(d) * cdiv(d->Cout, C5_BN);
+  const int mi = conv5_mi(d);
+  if (mode == 2 && d->out_mode == UNET_OUT_F32 && d->Cout > C5_BN && mi == C5_MI) return false;
+  const long long work = conv5_mtiles(d, mi) * cdiv(d->Cout, C5_BN);
   return work >= 256;
 }
 
@@ -968,7 +983,7 @@ int conv5_splitk(const unet_conv_desc* d) {
   const int on = e ? atoi(e) : 1;
   if (!on || conv5_mode() == 0 || d->act_out || !conv5_shape_ok(d)) return 1;
   if (d->Cout > 1024 || (d->Cout & (d->Cout - 1))) return 1;     // the finisher's channel-vector layout
-  const long long work = conv5_mtiles(d) * cdiv(d->Cout, C5_BN);
+  const long long work = conv5_mtiles(d, conv5_mi(d)) * cdiv(d->Cout, C5_BN);
   if (work >= 256) return 1;
   const int nch = cdiv(d->Cin, 16);
   int S = 1;
@@ -993,7 +1008,7 @@ static int fin_rows(const unet_conv_desc* d) {
 
 int conv5_stats_rows(const unet_conv_desc* d) {
   if (!conv5_eligible(d) && conv5_splitk(d) > 1) return fin_rows(d);
-  return conv5_gx(d) * C5_WM;
+  return conv5_gx(d, conv5_mi(d)) * C5_WM;
 }
 
 // can the forward write src[0]'s transformed input to act_out (the y-mode BN-activation kernel serves d)?
@@ -1004,8 +1019,9 @@ bool conv5_act_out_ok(const unet_conv_desc* d) {
 
 int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
   const int S = conv5_eligible(d) ? 1 : conv5_splitk(d);
-  if (S > 1) snprintf(buf, len, "conv5_kernel<%s,%d>+splitk%d", d->dtype == UNET_F16 ? "fp16" : "bf16", C5_MI, S);
-  else snprintf(buf, len, "conv5_kernel<%s,%d>", d->dtype == UNET_F16 ? "fp16" : "bf16", C5_MI);
+  const int mi = conv5_mi(d);
+  if (S > 1) snprintf(buf, len, "conv5_kernel<%s,%d>+splitk%d", d->dtype == UNET_F16 ? "fp16" : "bf16", mi, S);
+  else snprintf(buf, len, "conv5_kernel<%s,%d>", d->dtype == UNET_F16 ? "fp16" : "bf16", mi);
   return 0;
 }
 
@@ -1017,18 +1033,25 @@ int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
 // The 8-wave form (NWV 8).  The one-wave-per-SIMD form (NWV 4: 64 channels per wave, 12 LDS reads per 24 MFMAs
 // per tap column, 462-502 registers, no spills) measured 10-25 % slower on every layer
 // (profiles/r04_layerprof_conv5_{8,4}waves.txt): one wave cannot cover its own LDS and DMA latencies.
-template <typename T, int OM, int SK, int GATE, int ABL = 0, int PIPE_ = -1>
-static int launch5(const unet_conv_desc* d, hipStream_t st) {
-  constexpr int TH = C5_WM * C5_MI;
+template <typename T, int OM, int SK, int GATE, int ABL, int PIPE_, int MI>
+static int launch5_mi(const unet_conv_desc* d, hipStream_t st) {
+  constexpr int TH = C5_WM * MI;
   constexpr int PIPE = PIPE_ >= 0 ? PIPE_ : (OM == OM5_BNB && SK != SK_PLAIN && SK != SK5_PLAIN1) ? 0 : 1;
   const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH);
   const int mt = d->N * tw * th;
   const int gy = cdiv(d->Cout, C5_BN);
-  const int gx = conv5_gx(d);
+  const int gx = conv5_gx(d, MI);
   const int nch = cdiv(d->Cin, 16);
-  hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM, SK, GATE, ABL, PIPE, 8>), dim3(gx, gy), dim3(512), 0, st, *d, tw, th,
+  hipLaunchKernelGGL((conv5_kernel<T, MI, OM, SK, GATE, ABL, PIPE, 8>), dim3(gx, gy), dim3(512), 0, st, *d, tw, th,
                      mt, nch, nch);
   return check_launch("conv5");
+}
+template <typename T, int OM, int SK, int GATE, int ABL = 0, int PIPE_ = -1>
+static int launch5(const unet_conv_desc* d, hipStream_t st) {
+  if constexpr (ABL == 0) {
+    if (conv5_mi(d) == C5_MI_S) return launch5_mi<T, OM, SK, GATE, 0, PIPE_, C5_MI_S>(d, st);
+  }
+  return launch5_mi<T, OM, SK, GATE, ABL, PIPE_, C5_MI>(d, st);
 }
 
 template <typename T, int MODE>
@@ -1049,9 +1072,9 @@ static int launch5_finish(const unet_conv_desc* d, int S, hipStream_t st) {
 }
 
 // split-K: the conv into S fp32 slabs (one workgroup per tile and split), then the finisher
-template <typename T, int SK, int GATE>
-static int launch5_split(const unet_conv_desc* d, int S, hipStream_t st) {
-  constexpr int TH = C5_WM * C5_MI;
+template <typename T, int SK, int GATE, int MI>
+static int launch5_split_mi(const unet_conv_desc* d, int S, hipStream_t st) {
+  constexpr int TH = C5_WM * MI;
   if (!d->workspace) {
     set_error("unet_conv: this descriptor runs split-K and needs d->workspace (unet_conv_workspace bytes)");
     return UNET_ERR_ARG;
@@ -1069,10 +1092,14 @@ static int launch5_split(const unet_conv_desc* d, int S, hipStream_t st) {
   k.stats = nullptr;
   k.bnb_stats = nullptr;
   k.act_out = nullptr;
-  hipLaunchKernelGGL((conv5_kernel<T, C5_MI, OM5_F32, SK, GATE, 0, 1, 8, true>), dim3(mt, gy, S), dim3(512), 0, st, k,
+  hipLaunchKernelGGL((conv5_kernel<T, MI, OM5_F32, SK, GATE, 0, 1, 8, true>), dim3(mt, gy, S), dim3(512), 0, st, k,
                      tw, th, mt, nch / S, nch);
   if (int e = check_launch("conv5 split")) return e;
   return launch5_finish<T>(d, S, st);
+}
+template <typename T, int SK, int GATE>
+static int launch5_split(const unet_conv_desc* d, int S, hipStream_t st) {
+  return conv5_mi(d) == C5_MI_S ? launch5_split_mi<T, SK, GATE, C5_MI_S>(d, S, st) : launch5_split_mi<T, SK, GATE, C5_MI>(d, S, st);
 }
 
 // source kind of a descriptor: plain, one BN activation (gated or not), or a BN activation + a stored map.
@@ -1131,9 +1158,9 @@ static int abl5(const unet_conv_desc* d, int abl, hipStream_t st) {
 }
 
 // split-K ablations: the split kernel alone (ABL bits as above) or, abl < 0, the y + BN-stats finisher alone
-template <int SK>
-static int abl5_split(const unet_conv_desc* d, int abl, hipStream_t st) {
-  constexpr int TH = C5_WM * C5_MI;
+template <int SK, int MI>
+static int abl5_split_mi(const unet_conv_desc* d, int abl, hipStream_t st) {
+  constexpr int TH = C5_WM * MI;
   const int S = conv5_splitk(d);
   const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH), mt = d->N * tw * th, gy = cdiv(d->Cout, C5_BN);
   const int nch = cdiv(d->Cin, 16);
@@ -1152,7 +1179,7 @@ static int abl5_split(const unet_conv_desc* d, int abl, hipStream_t st) {
   k.bnb_stats = nullptr;
   k.act_out = nullptr;
   const dim3 grid(mt, gy, S);
-#define C5SA(A) hipLaunchKernelGGL((conv5_kernel<bf16, C5_MI, OM5_F32, SK, 0, A, 1, 8, true>), grid, dim3(512), 0, st, k, tw, th, mt, nch / S, nch)
+#define C5SA(A) hipLaunchKernelGGL((conv5_kernel<bf16, MI, OM5_F32, SK, 0, A, 1, 8, true>), grid, dim3(512), 0, st, k, tw, th, mt, nch / S, nch)
   switch (abl) {
     case 0: C5SA(0); break;
     case 1: C5SA(1); break;
@@ -1166,6 +1193,10 @@ static int abl5_split(const unet_conv_desc* d, int abl, hipStream_t st) {
   }
 #undef C5SA
   return check_launch("conv5 split (diag)");
+}
+template <int SK>
+static int abl5_split(const unet_conv_desc* d, int abl, hipStream_t st) {
+  return conv5_mi(d) == C5_MI_S ? abl5_split_mi<SK, C5_MI_S>(d, abl, st) : abl5_split_mi<SK, C5_MI>(d, abl, st);
 }
 
 }  // namespace unet
