@@ -193,6 +193,22 @@ int unet_bn_bwd_finalize(const float* sum_g, const float* sum_gx, int rows, int 
                          float* dbeta, int accum, float* coef, void* stream);
 /* column sums of a [rows][C] fp32 partial table (fp64 accumulation): out (+)= sum_r part[r][:]    */
 int unet_colsum(const float* part, int rows, int C, float* out, int accum, void* stream);
+/* Several independent finalizes in ONE launch (round 5: the attention gate's W_g / W_x BatchNorms,
+ * whose statistics are ready together).  Each job has exactly the arguments (and results) of one
+ * unet_bn_finalize / unet_bn_bwd_finalize call; a backward job with gamma == NULL and coef == NULL is
+ * a column sum into dbeta (unet_colsum).  count <= UNET_BN_MULTI_MAX.                                 */
+#define UNET_BN_MULTI_MAX 4
+typedef struct unet_bn_finalize_job {
+  const float* stats; int rows, C; long long count; const float* gamma; const float* beta;
+  float* running_mean; float* running_var; long long* num_batches_tracked; float momentum, eps;
+  float* mean; float* invstd; float* scale; float* shift;
+} unet_bn_finalize_job;
+int unet_bn_finalize_multi(int count, const unet_bn_finalize_job* jobs, void* stream);
+typedef struct unet_bn_bwd_finalize_job {
+  const float* sum_g; const float* sum_gx; int rows, C; long long count; const float* gamma;
+  const float* mean; const float* invstd; float* dgamma; float* dbeta; int accum; float* coef;
+} unet_bn_bwd_finalize_job;
+int unet_bn_bwd_finalize_multi(int count, const unet_bn_bwd_finalize_job* jobs, void* stream);
 /* dy (op dtype) = A*g + B*y + Cc                                                                */
 int unet_bn_bwd_apply(int dtype, int da_dtype, long long P, int C, const void* da, const void* y,
                       const float* scale, const float* shift, int relu, const float* coef, void* dy, void* stream);

@@ -945,3 +945,82 @@ def test_pack_weights_batched_matches_single(prec):
     torch.cuda.synchronize()
     for (o, _), r in zip(outs, refs):
         assert torch.equal(o.view(torch.int16), r.view(torch.int16))
+
+
+def test_bn_finalize_multi_matches_single():
+    """unet_bn_finalize_multi / unet_bn_bwd_finalize_multi (round 5: the attention gate's two projections
+    finalized in one launch) against one unet_bn_finalize / unet_bn_bwd_finalize call per job: bit-identical,
+    running statistics and num_batches_tracked included; the column-sum job against fp64 (unet_colsum's role)."""
+    L, R = _lib(), _rt()
+    torch.manual_seed(5)
+    dev = "cuda"
+    shapes = [(32, 2048, 4 * 512 * 512), (64, 1024, 4 * 256 * 256), (3, 7, 100)]
+    fwd = {}
+    for mode in ("single", "multi"):
+        outs, jobs, keep = [], [], []
+        for k, (C, rows, cnt) in enumerate(shapes):
+            g = torch.Generator(device="cpu").manual_seed(100 + k)
+            stats = torch.stack([torch.randn(C, rows, generator=g) * 3 + 1,
+                                 torch.rand(C, rows, generator=g) * 10 + 5]).to(dev)
+            gamma, beta = torch.randn(C, generator=g).to(dev), torch.randn(C, generator=g).to(dev)
+            rm, rv = torch.randn(C, generator=g).to(dev), torch.rand(C, generator=g).to(dev) + 0.5
+            nbt = torch.tensor([3], dtype=torch.int64, device=dev)
+            o = [torch.empty(C, device=dev) for _ in range(4)]
+            keep += [stats, gamma, beta]
+            mom = 0.1 if k != 1 else -1.0     # momentum=None: the cumulative average reads num_batches_tracked
+            if mode == "single":
+                L.call("unet_bn_finalize", stats.data_ptr(), rows, C, cnt, gamma.data_ptr(), beta.data_ptr(),
+                       rm.data_ptr(), rv.data_ptr(), nbt.data_ptr(), mom, 1e-5, o[0].data_ptr(), o[1].data_ptr(),
+                       o[2].data_ptr(), o[3].data_ptr(), R.stream())
+            else:
+                j = L.BnFinJob()
+                j.stats, j.rows, j.C, j.count, j.gamma, j.beta = stats.data_ptr(), rows, C, cnt, gamma.data_ptr(), beta.data_ptr()
+                j.running_mean, j.running_var, j.num_batches_tracked = rm.data_ptr(), rv.data_ptr(), nbt.data_ptr()
+                j.momentum, j.eps = mom, 1e-5
+                j.mean, j.invstd, j.scale, j.shift = (t.data_ptr() for t in o)
+                jobs.append(j)
+            outs.append(o + [rm, rv, nbt])
+        if mode == "multi":
+            L.call("unet_bn_finalize_multi", len(jobs), (L.BnFinJob * len(jobs))(*jobs), R.stream())
+        torch.cuda.synchronize()
+        fwd[mode] = outs
+    for a, b in zip(fwd["single"], fwd["multi"]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    # backward: two BN jobs (as the gate's) and a column sum
+    C, rows, P = 32, 2048, 4 * 512 * 512
+    g = torch.Generator(device="cpu").manual_seed(7)
+    part = (torch.randn(4, rows, C, generator=g) * 2).to(dev)
+    gam = [torch.randn(C, generator=g).to(dev) for _ in range(2)]
+    mu = [torch.randn(C, generator=g).to(dev) for _ in range(2)]
+    ist = [torch.rand(C, generator=g).to(dev) + 0.5 for _ in range(2)]
+    res = {}
+    for mode in ("single", "multi"):
+        o = [[torch.empty(C, device=dev), torch.empty(C, device=dev), torch.empty(3, C, device=dev)] for _ in range(2)]
+        cs = torch.empty(C, device=dev)
+        if mode == "single":
+            for k in range(2):
+                L.call("unet_bn_bwd_finalize", part[0].data_ptr(), part[1 + k].data_ptr(), rows, C, P, gam[k].data_ptr(),
+                       mu[k].data_ptr(), ist[k].data_ptr(), o[k][0].data_ptr(), o[k][1].data_ptr(), 0, o[k][2].data_ptr(),
+                       R.stream())
+            L.call("unet_colsum", part[3].data_ptr(), rows, C, cs.data_ptr(), 0, R.stream())
+        else:
+            jobs = []
+            for k in range(2):
+                j = L.BnBwdFinJob()
+                j.sum_g, j.sum_gx, j.rows, j.C, j.count = part[0].data_ptr(), part[1 + k].data_ptr(), rows, C, P
+                j.gamma, j.mean, j.invstd = gam[k].data_ptr(), mu[k].data_ptr(), ist[k].data_ptr()
+                j.dgamma, j.dbeta, j.accum, j.coef = o[k][0].data_ptr(), o[k][1].data_ptr(), 0, o[k][2].data_ptr()
+                jobs.append(j)
+            j = L.BnBwdFinJob()
+            j.sum_g, j.sum_gx, j.rows, j.C, j.count, j.dbeta = part[3].data_ptr(), None, rows, C, 0, cs.data_ptr()
+            jobs.append(j)
+            L.call("unet_bn_bwd_finalize_multi", len(jobs), (L.BnBwdFinJob * len(jobs))(*jobs), R.stream())
+        torch.cuda.synchronize()
+        res[mode] = (o, cs)
+    for k in range(2):
+        for x, y in zip(res["single"][0][k], res["multi"][0][k]):
+            assert torch.equal(x, y)
+    ref = part[3].double().sum(0)
+    for cs in (res["single"][1], res["multi"][1]):
+        assert ((cs.double() - ref).abs() <= 1e-6 * part[3].double().abs().sum(0) + 1e-6).all()

@@ -47,12 +47,11 @@ static inline int fin_threads(int rows) {
   return t < 64 ? 64 : (t > 1024 ? 1024 : t);
 }
 
-// one block per channel
-__global__ void bn_finalize_kernel(const float* stats, int rows, int C, long long count, const float* gamma,
-                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
-                                   float eps, float* mean, float* invstd, float* scale, float* shift) {
-  __shared__ double sh2[32];
-  const int c = blockIdx.x;
+// one block per channel (the body shared by the single and the batched launch)
+__device__ __forceinline__ void bn_finalize_body(const float* stats, int rows, int C, long long count,
+                                                 const float* gamma, const float* beta, float* rmean, float* rvar,
+                                                 long long* nbt, float momentum, float eps, float* mean, float* invstd,
+                                                 float* scale, float* shift, int c, double* sh2) {
   // the per-channel operands of the epilogue, loaded before the partial rows (in flight together: the kernel is
   // a chain of dependent memory round trips, and these need not be one of them)
   float g_ = 0.f, b_ = 0.f, rm_ = 0.f, rv_ = 0.f;
@@ -100,6 +99,30 @@ __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long lon
     }
     if (c == 0 && nbt) *nbt += 1;
   }
+}
+
+__global__ void bn_finalize_kernel(const float* stats, int rows, int C, long long count, const float* gamma,
+                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
+                                   float eps, float* mean, float* invstd, float* scale, float* shift) {
+  __shared__ double sh2[32];
+  bn_finalize_body(stats, rows, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, mean, invstd, scale, shift,
+                   (int)blockIdx.x, sh2);
+}
+
+// the batched form: blocks [c0[k], c0[k+1]) serve job k (block-uniform)
+struct BnFinJobs {
+  unet_bn_finalize_job j[UNET_BN_MULTI_MAX];
+  int c0[UNET_BN_MULTI_MAX + 1];
+  int n;
+};
+__global__ void bn_finalize_multi_kernel(const BnFinJobs js) {
+  __shared__ double sh2[32];
+  int k = 0;
+  while (k + 1 < js.n && (int)blockIdx.x >= js.c0[k + 1]) ++k;
+  const unet_bn_finalize_job& jb = js.j[k];
+  bn_finalize_body(jb.stats, jb.rows, jb.C, jb.count, jb.gamma, jb.beta, jb.running_mean, jb.running_var,
+                   jb.num_batches_tracked, jb.momentum, jb.eps, jb.mean, jb.invstd, jb.scale, jb.shift,
+                   (int)blockIdx.x - js.c0[k], sh2);
 }
 
 // eval mode: the running-statistics affine; mean / invstd (optional) are what the backward of an eval-mode
@@ -392,13 +415,13 @@ static inline int reduce_rows_vec(long long P, int C) {
 }
 
 // one block per channel: sums over rows in fp64.  count == 0: eval mode (running statistics are constants
-// of the forward), so dy = γ·invstd·g: coef = (γ·invstd, 0, 0)
-__global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
-                                       const float* gamma, const float* mean, const float* invstd, float* dgamma,
-                                       float* dbeta, int accum, float* coef) {
-  __shared__ double sh2[32];
-  const int c = blockIdx.x;
-  // the epilogue's per-channel operands, in flight with the partial rows (as bn_finalize_kernel)
+// of the forward), so dy = γ·invstd·g: coef = (γ·invstd, 0, 0).  (The body shared by the single and the
+// batched launch; with coef == NULL and dgamma == NULL it is a column sum of sum_g into dbeta.)
+__device__ __forceinline__ void bn_bwd_finalize_body(const float* sum_g, const float* sum_gx, int rows, int C,
+                                                     long long count, const float* gamma, const float* mean,
+                                                     const float* invstd, float* dgamma, float* dbeta, int accum,
+                                                     float* coef, int c, double* sh2) {
+  // the epilogue's per-channel operands, in flight with the partial rows (as bn_finalize_body)
   float g_ = 0.f, is_ = 0.f, mu_ = 0.f, dg_ = 0.f, db_ = 0.f;
   if (threadIdx.x == 0) {
     if (coef) {
@@ -411,20 +434,23 @@ __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, 
       if (dbeta) db_ = dbeta[c];
     }
   }
+  const bool two = sum_gx && (dgamma || coef);   // a column-sum job reads one table
   double a = 0, b = 0;
   const int B = blockDim.x;
   int r = threadIdx.x;
   for (; r + 3 * B < rows; r += 4 * B) {  // 4 independent loads per trip, adds in row order
     const float g0 = sum_g[(size_t)r * C + c], g1 = sum_g[(size_t)(r + B) * C + c];
     const float g2 = sum_g[(size_t)(r + 2 * B) * C + c], g3 = sum_g[(size_t)(r + 3 * B) * C + c];
-    const float x0 = sum_gx[(size_t)r * C + c], x1 = sum_gx[(size_t)(r + B) * C + c];
-    const float x2 = sum_gx[(size_t)(r + 2 * B) * C + c], x3 = sum_gx[(size_t)(r + 3 * B) * C + c];
     a += g0; a += g1; a += g2; a += g3;
-    b += x0; b += x1; b += x2; b += x3;
+    if (two) {
+      const float x0 = sum_gx[(size_t)r * C + c], x1 = sum_gx[(size_t)(r + B) * C + c];
+      const float x2 = sum_gx[(size_t)(r + 2 * B) * C + c], x3 = sum_gx[(size_t)(r + 3 * B) * C + c];
+      b += x0; b += x1; b += x2; b += x3;
+    }
   }
   for (; r < rows; r += B) {
     a += sum_g[(size_t)r * C + c];
-    b += sum_gx[(size_t)r * C + c];
+    if (two) b += sum_gx[(size_t)r * C + c];
   }
   block_sum2_d(a, b, sh2);
   if (threadIdx.x == 0) {
@@ -444,6 +470,28 @@ __global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, 
       }
     }
   }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* sum_g, const float* sum_gx, int rows, int C, long long count,
+                                       const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                                       float* dbeta, int accum, float* coef) {
+  __shared__ double sh2[32];
+  bn_bwd_finalize_body(sum_g, sum_gx, rows, C, count, gamma, mean, invstd, dgamma, dbeta, accum, coef,
+                       (int)blockIdx.x, sh2);
+}
+
+struct BnBwdFinJobs {
+  unet_bn_bwd_finalize_job j[UNET_BN_MULTI_MAX];
+  int c0[UNET_BN_MULTI_MAX + 1];
+  int n;
+};
+__global__ void bn_bwd_finalize_multi_kernel(const BnBwdFinJobs js) {
+  __shared__ double sh2[32];
+  int k = 0;
+  while (k + 1 < js.n && (int)blockIdx.x >= js.c0[k + 1]) ++k;
+  const unet_bn_bwd_finalize_job& jb = js.j[k];
+  bn_bwd_finalize_body(jb.sum_g, jb.sum_gx, jb.rows, jb.C, jb.count, jb.gamma, jb.mean, jb.invstd, jb.dgamma,
+                       jb.dbeta, jb.accum, jb.coef, (int)blockIdx.x - js.c0[k], sh2);
 }
 
 template <typename T, typename G>
@@ -490,6 +538,56 @@ int unet_bn_finalize(const float* stats, int rows, int C, long long count, const
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(fin_threads(rows)), 0, (hipStream_t)stream, stats, rows, C, count, gamma,
                      beta, running_mean, running_var, nbt, momentum, eps, mean, invstd, scale, shift);
   return check_launch("bn_finalize");
+}
+
+int unet_bn_finalize_multi(int count, const unet_bn_finalize_job* jobs, void* stream) {
+  if (count < 1 || count > UNET_BN_MULTI_MAX || !jobs) {
+    set_error("unet_bn_finalize_multi: 1..UNET_BN_MULTI_MAX jobs");
+    return UNET_ERR_ARG;
+  }
+  BnFinJobs js{};
+  js.n = count;
+  int rows_max = 1;
+  js.c0[0] = 0;
+  for (int k = 0; k < count; ++k) {
+    const unet_bn_finalize_job& j = jobs[k];
+    if (!j.stats || j.rows <= 0 || j.C <= 0 || j.count <= 0 || !j.gamma || !j.beta || !j.mean || !j.invstd || !j.scale ||
+        !j.shift) {
+      set_error("unet_bn_finalize_multi: bad job");
+      return UNET_ERR_ARG;
+    }
+    js.j[k] = j;
+    js.c0[k + 1] = js.c0[k] + j.C;
+    rows_max = j.rows > rows_max ? j.rows : rows_max;
+  }
+  hipLaunchKernelGGL(bn_finalize_multi_kernel, dim3(js.c0[count]), dim3(fin_threads(rows_max)), 0, (hipStream_t)stream, js);
+  return check_launch("bn_finalize_multi");
+}
+
+int unet_bn_bwd_finalize_multi(int count, const unet_bn_bwd_finalize_job* jobs, void* stream) {
+  if (count < 1 || count > UNET_BN_MULTI_MAX || !jobs) {
+    set_error("unet_bn_bwd_finalize_multi: 1..UNET_BN_MULTI_MAX jobs");
+    return UNET_ERR_ARG;
+  }
+  BnBwdFinJobs js{};
+  js.n = count;
+  int rows_max = 1;
+  js.c0[0] = 0;
+  for (int k = 0; k < count; ++k) {
+    const unet_bn_bwd_finalize_job& j = jobs[k];
+    const bool colsum = !j.coef && !j.dgamma;
+    if (!j.sum_g || j.rows <= 0 || j.C <= 0 || j.count < 0 || (!colsum && !j.sum_gx) ||
+        (j.coef && (!j.gamma || !j.invstd || (j.count > 0 && !j.mean))) || (colsum && !j.dbeta)) {
+      set_error("unet_bn_bwd_finalize_multi: bad job");
+      return UNET_ERR_ARG;
+    }
+    js.j[k] = j;
+    js.c0[k + 1] = js.c0[k] + j.C;
+    rows_max = j.rows > rows_max ? j.rows : rows_max;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_multi_kernel, dim3(js.c0[count]), dim3(fin_threads(rows_max)), 0, (hipStream_t)stream,
+                     js);
+  return check_launch("bn_bwd_finalize_multi");
 }
 
 int unet_bn_eval_affine(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,

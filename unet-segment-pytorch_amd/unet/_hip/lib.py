@@ -43,6 +43,20 @@ class PackJob(ctypes.Structure):
 PACK_MAX_JOBS = 64
 
 
+class BnFinJob(ctypes.Structure):      # unet_bn_finalize_job
+    _fields_ = [("stats", c_vp), ("rows", c_int), ("C", c_int), ("count", c_ll), ("gamma", c_vp), ("beta", c_vp),
+                ("running_mean", c_vp), ("running_var", c_vp), ("num_batches_tracked", c_vp), ("momentum", c_float),
+                ("eps", c_float), ("mean", c_vp), ("invstd", c_vp), ("scale", c_vp), ("shift", c_vp)]
+
+
+class BnBwdFinJob(ctypes.Structure):   # unet_bn_bwd_finalize_job
+    _fields_ = [("sum_g", c_vp), ("sum_gx", c_vp), ("rows", c_int), ("C", c_int), ("count", c_ll), ("gamma", c_vp),
+                ("mean", c_vp), ("invstd", c_vp), ("dgamma", c_vp), ("dbeta", c_vp), ("accum", c_int), ("coef", c_vp)]
+
+
+BN_MULTI_MAX = 4
+
+
 class WgradDesc(ctypes.Structure):
     _fields_ = [("dtype", c_int), ("N", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int),
                 ("ksize", c_int), ("nsrc", c_int), ("src", Src * 2), ("dy", c_vp), ("dw", c_vp), ("accum", c_int),
@@ -77,6 +91,8 @@ _SIGS = {
     "unet_bn_bwd_apply_pool": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
                                        c_vp, c_int, c_vp, c_vp, c_vp]),
     "unet_colsum": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp]),
+    "unet_bn_finalize_multi": (c_int, [c_int, ctypes.POINTER(BnFinJob), c_vp]),
+    "unet_bn_bwd_finalize_multi": (c_int, [c_int, ctypes.POINTER(BnBwdFinJob), c_vp]),
     "unet_gate_psi_rows": (c_int, [c_ll]),
     "unet_gate_psi": (c_int, [c_int, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "unet_gate_psi_eval": (c_int, [c_int, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,

@@ -188,7 +188,7 @@ class Act:
     for a single-consumer activation in bf16 mode (`grad_single`)."""
 
     __slots__ = ("data", "N", "H", "W", "C", "ab", "relu", "mean", "invstd", "grad", "_grad_init", "keep",
-                 "bn_owned", "pool_grad", "batch_stats", "oc_fused")
+                 "bn_owned", "pool_grad", "batch_stats", "oc_fused", "fin_job")
 
     def __init__(self, data: torch.Tensor, ab: Optional[torch.Tensor], relu: bool,
                  mean: Optional[torch.Tensor] = None, invstd: Optional[torch.Tensor] = None):
@@ -209,6 +209,8 @@ class Act:
         # set by OutConvStage.backward when OutConv is the only consumer: (dl, w, K, bn partial sums, rows) — the
         # gradient W^T dl is recomputed by the BN-backward apply instead of being stored
         self.oc_fused = None
+        # set by ConvBN.forward(defer_fin=True): (unet_bn_finalize_job, its partial sums) until finalize_many runs it
+        self.fin_job = None
 
     @property
     def scale(self):

@@ -40,6 +40,26 @@ def _materialize(prec: Precision, src: L.Src, N: int, H: int, W: int) -> torch.T
     return out
 
 
+def finalize_many(acts) -> None:
+    """Launch the deferred batch-statistics finalizes of several activations (ConvBN.forward(defer_fin=True))
+    as one unet_bn_finalize_multi launch: the same per-channel work and results as one unet_bn_finalize each."""
+    jobs = [a.fin_job for a in acts if getattr(a, "fin_job", None) is not None]
+    for i in range(0, len(jobs), L.BN_MULTI_MAX):
+        chunk = jobs[i:i + L.BN_MULTI_MAX]
+        arr = (L.BnFinJob * len(chunk))(*[j for j, _ in chunk])
+        L.call("unet_bn_finalize_multi", len(chunk), arr, stream())
+    for a in acts:
+        a.fin_job = None
+
+
+def _bwd_fin_job(sum_g, sum_gx, rows, C, count, gamma, mean, invstd, dgamma, dbeta, coef) -> L.BnBwdFinJob:
+    j = L.BnBwdFinJob()
+    j.sum_g, j.sum_gx, j.rows, j.C, j.count = vp(sum_g), vp(sum_gx), rows, C, count
+    j.gamma, j.mean, j.invstd = vp(gamma), vp(mean), vp(invstd)
+    j.dgamma, j.dbeta, j.accum, j.coef = vp(dgamma), vp(dbeta), 0, vp(coef)
+    return j
+
+
 def _plain_src(t: torch.Tensor) -> L.Src:
     s = L.Src()
     s.kind = L.SRC_PLAIN
@@ -75,7 +95,9 @@ class ConvBN:
 
     # ---- forward ----
     def forward(self, prec: Precision, srcs: List[L.Src], N: int, H: int, W: int, training: bool,
-                keep=None) -> Act:
+                keep=None, defer_fin: bool = False) -> Act:
+        """defer_fin: the batch-statistics finalize is not launched here but left on the result as
+        `a.fin_job` (an unet_bn_finalize_job) for the caller to launch with others (`finalize_many`)."""
         dev = self.conv.weight.device
         wp = self.pre_wp if self.pre_wp is not None else pack_weight(self.conv.weight, prec, transpose=False)
         self.pre_wp = None
@@ -106,13 +128,25 @@ class ConvBN:
                      lambda: L.call("unet_conv", d, stream()), d.out_mode)
         mean = f32(self.cout, device=dev)
         invstd = f32(self.cout, device=dev)
+        fin_job = None
         if use_batch:
             upd = training and bn.track_running_stats
             mom = -1.0 if bn.momentum is None else float(bn.momentum)
-            L.call("unet_bn_finalize", vp(stats), mt, self.cout, N * H * W, vp(bn.weight), vp(bn.bias),
-                   vp(bn.running_mean) if upd else None, vp(bn.running_var) if upd else None,
-                   vp(bn.num_batches_tracked) if upd else None, mom, float(bn.eps), vp(mean), vp(invstd),
-                   vp(ab[0]), vp(ab[1]), stream())
+            if defer_fin:
+                j = L.BnFinJob()
+                j.stats, j.rows, j.C, j.count = vp(stats), mt, self.cout, N * H * W
+                j.gamma, j.beta = vp(bn.weight), vp(bn.bias)
+                j.running_mean = vp(bn.running_mean) if upd else None
+                j.running_var = vp(bn.running_var) if upd else None
+                j.num_batches_tracked = vp(bn.num_batches_tracked) if upd else None
+                j.momentum, j.eps = mom, float(bn.eps)
+                j.mean, j.invstd, j.scale, j.shift = vp(mean), vp(invstd), vp(ab[0]), vp(ab[1])
+                fin_job = (j, stats)   # the job holds raw pointers: keep the partial sums alive until it runs
+            else:
+                L.call("unet_bn_finalize", vp(stats), mt, self.cout, N * H * W, vp(bn.weight), vp(bn.bias),
+                       vp(bn.running_mean) if upd else None, vp(bn.running_var) if upd else None,
+                       vp(bn.num_batches_tracked) if upd else None, mom, float(bn.eps), vp(mean), vp(invstd),
+                       vp(ab[0]), vp(ab[1]), stream())
         else:
             # eval mode (running statistics): mean / invstd are the running ones, which the backward of an
             # eval-mode forward treats as constants (unet_bn_bwd_finalize with count 0)
@@ -122,6 +156,7 @@ class ConvBN:
         a.batch_stats = use_batch
         a.keep = keep  # keeps the source tensors alive until backward
         a.bn_owned = True
+        a.fin_job = fin_job
         return a
 
     # ---- backward ----
@@ -315,9 +350,11 @@ class GateStage:
             return
         # bilinear(g -> x size) (layers.py:183): the Up stage's materialised map when it is the same one
         self.src_g = g_up if g_up is not None else g.src_up(H, W, 0, 0)
-        self.gw = self.cg.forward(prec, [self.src_g], N, H, W, training)
+        # the two projections' BatchNorm finalizes are independent: one launch after both convs (round 5)
+        self.gw = self.cg.forward(prec, [self.src_g], N, H, W, training, defer_fin=True)
         self.gw_src = [self.src_g]
-        self.xw = self.cx.forward(prec, [x.src()], N, H, W, training)
+        self.xw = self.cx.forward(prec, [x.src()], N, H, W, training, defer_fin=True)
+        finalize_many([self.gw, self.xw])
         P = N * H * W
         self.p = f32(N, H, W, device=dev)
         rows = L.load().unet_gate_psi_rows(P)
@@ -397,18 +434,18 @@ class GateStage:
                vp(self.wpsi), vp(dq), vp(self.p), vp(pcoef), vp(part2), stream())
         dgg, dbg, gcoef = f32(Ci, device=dev), f32(Ci, device=dev), f32(3, Ci, device=dev)
         dgx, dbx, xcoef = f32(Ci, device=dev), f32(Ci, device=dev), f32(3, Ci, device=dev)
-        L.call("unet_bn_bwd_finalize", vp(part2[0]), vp(part2[1]), rows2, Ci, P if self.gw.batch_stats else 0,
-               vp(self.cg.bn.weight),
-               vp(self.gw.mean), vp(self.gw.invstd), vp(dgg), vp(dbg), 0, vp(gcoef), stream())
-        L.call("unet_bn_bwd_finalize", vp(part2[0]), vp(part2[2]), rows2, Ci, P if self.xw.batch_stats else 0,
-               vp(self.cx.bn.weight),
-               vp(self.xw.mean), vp(self.xw.invstd), vp(dgx), vp(dbx), 0, vp(xcoef), stream())
+        dwpsi = f32(Ci, device=dev)
+        # both projections' BN-backward finalizes and psi's weight gradient (a column sum) in one launch (round 5)
+        jobs = [_bwd_fin_job(part2[0], part2[1], rows2, Ci, P if self.gw.batch_stats else 0, self.cg.bn.weight,
+                             self.gw.mean, self.gw.invstd, dgg, dbg, gcoef),
+                _bwd_fin_job(part2[0], part2[2], rows2, Ci, P if self.xw.batch_stats else 0, self.cx.bn.weight,
+                             self.xw.mean, self.xw.invstd, dgx, dbx, xcoef),
+                _bwd_fin_job(part2[3], None, rows2, Ci, 0, None, None, None, None, dwpsi, None)]
+        L.call("unet_bn_bwd_finalize_multi", len(jobs), (L.BnBwdFinJob * len(jobs))(*jobs), stream())
         grads.put(self.cg.bn.weight, dgg)
         grads.put(self.cg.bn.bias, dbg)
         grads.put(self.cx.bn.weight, dgx)
         grads.put(self.cx.bn.bias, dbx)
-        dwpsi = f32(Ci, device=dev)
-        L.call("unet_colsum", vp(part2[3]), rows2, Ci, vp(dwpsi), 0, stream())
         grads.put(self.psi_conv.weight, dwpsi.view(1, Ci, 1, 1))
         # (3) dgw, dxw
         dgw = torch.empty(x.N, x.H, x.W, Ci, dtype=prec.torch_dtype, device=dev)
