@@ -590,51 +590,63 @@ __global__ __launch_bounds__(256) void smallcin_wgrad_mfma_kernel(const unet_wgr
     }
 }
 
-// dW[co][kk] (+)= Σ_rows part[row][co][kk] + part[row][co][kk + K9]  (fixed order).  One block per output
-// channel co: a thread reads whole 2·K9-float row segments of its rows (contiguous, 8-byte aligned), keeps K9
-// running sums, then the block adds the 256 threads' sums in a fixed tree.  (Round 5: one block per output
-// column read one float per row at a 4.6 KB stride — 2 x 2048 scattered loads per column, 17.9 us per step.)
-template <int K9>   // 9 * Cin
-__global__ __launch_bounds__(256) void smallcin_fold_kernel(const float* part, int rows, int Cout, float* dw, int accum) {
-  __shared__ float red[256];   // one kk at a time
-  constexpr int K2 = 2 * K9;
-  const int co = blockIdx.x, tid = threadIdx.x;
-  float s[K9];
+// dW[co][kk] (+)= Σ_rows part[row][co][kk] + part[row][co][kk + K9]  (fixed order), in two coalesced passes
+// over the [rows][W = Cout·2·K9] partial table: pass 1 — block b sums its SCF_R consecutive rows for every column
+// (consecutive threads, consecutive columns), pass 2 — one thread per output column adds the blocks' sums in
+// block order and folds the x_hi / x_lo halves.  (Round 5: the one-pass fold, one block per output column or
+// per output channel, read one column of the 2048-row table at a 4.6 KB stride per row: 18-20 us per step.)
+constexpr int SCF_R = 8;     // rows per pass-1 block (2048 rows: 256 blocks)
+constexpr int SCF_KL = 32;   // pass 2: lanes over the pass-1 blocks (x 8 output columns per block)
+template <int CIN>
+__global__ __launch_bounds__(256) void smallcin_fold1_kernel(const float* part, int rows, float* sums) {
+  constexpr int W = 64 * 18 * CIN, NC = (W + 255) / 256;
+  const int r0 = blockIdx.x * SCF_R;
+  float v[NC][SCF_R];
 #pragma unroll
-  for (int k = 0; k < K9; ++k) s[k] = 0.f;
-  // 4 rows per trip, all their loads issued before the adds (each row's sums stay in row order)
-  int r = tid;
-  for (; r + 3 * 256 < rows; r += 4 * 256) {
-    float v[4][K2];
+  for (int j = 0; j < NC; ++j)
+#pragma unroll
+    for (int i = 0; i < SCF_R; ++i) {   // every load of the thread issued first (one memory round trip)
+      const int c = threadIdx.x + 256 * j, r = r0 + i;
+      v[j][i] = (c < W && r < rows) ? part[(size_t)r * W + c] : 0.f;
+    }
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = threadIdx.x + 256 * j;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < SCF_R; ++i) s += v[j][i];   // row order
+    if (c < W) sums[(size_t)blockIdx.x * W + c] = s;
+  }
+}
+template <int CIN>
+__global__ __launch_bounds__(256) void smallcin_fold2_kernel(const float* sums, int nb, float* dw, int accum) {
+  constexpr int K9 = 9 * CIN, W = 64 * 2 * K9;
+  __shared__ float red[2][SCF_KL][8];
+  const int cl = threadIdx.x & 7, kl = threadIdx.x >> 3;   // 8 output columns x 32 block lanes
+  const int col = blockIdx.x * 8 + cl;                    // output column (co, kk) of 64 * K9
+  const bool ok = col < 64 * K9;
+  const int co = ok ? col / K9 : 0, kk = ok ? col % K9 : 0;
+  const float* p = sums + (size_t)co * 2 * K9 + kk;
+  float a = 0.f, b = 0.f;
+  for (int k0 = kl; k0 < nb; k0 += 4 * SCF_KL) {   // 4 block rows per trip, loads first
+    float va[4], vb[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const float* p = part + ((size_t)(r + u * 256) * Cout + co) * K2;
-#pragma unroll
-      for (int k = 0; k < K2; ++k) v[u][k] = p[k];
+      const int k = k0 + u * SCF_KL;
+      va[u] = (ok && k < nb) ? p[(size_t)k * W] : 0.f;
+      vb[u] = (ok && k < nb) ? p[(size_t)k * W + K9] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int k = 0; k < K9; ++k) s[k] += v[u][k] + v[u][k + K9];
+    for (int u = 0; u < 4; ++u) { a += va[u]; b += vb[u]; }
   }
-  for (; r < rows; r += 256) {
-    const float* p = part + ((size_t)r * Cout + co) * K2;
-#pragma unroll
-    for (int k = 0; k < K9; ++k) s[k] += p[k] + p[k + K9];
-  }
-#pragma unroll
-  for (int k = 0; k < K9; ++k) {
-    red[tid] = s[k];
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) red[tid] += red[tid + o];
-      __syncthreads();
-    }
-    if (tid == 0) {
-      const int col = co * K9 + k;
-      dw[col] = accum ? dw[col] + red[0] : red[0];
-    }
-    __syncthreads();
+  red[0][kl][cl] = a;
+  red[1][kl][cl] = b;
+  __syncthreads();
+  if (kl == 0 && ok) {
+    float sa = 0.f, sb = 0.f;
+    for (int k = 0; k < SCF_KL; ++k) { sa += red[0][k][cl]; sb += red[1][k][cl]; }   // lane order
+    const float v = sa + sb;
+    dw[col] = accum ? dw[col] + v : v;
   }
 }
 
@@ -654,7 +666,10 @@ static int smallcin_wgrad_grid(const unet_wgrad_desc* d, int* tiles) {
 bool smallcin_wgrad_is_mfma(const unet_wgrad_desc* d) { return smallcin_wgrad_mfma_ok(d); }
 
 size_t smallcin_wgrad_ws(const unet_wgrad_desc* d) {
-  if (smallcin_wgrad_mfma_ok(d)) return (size_t)4 * smallcin_wgrad_grid(d, nullptr) * 64 * (2 * 9 * d->Cin) * sizeof(float);
+  if (smallcin_wgrad_mfma_ok(d)) {   // the partial table [4·grid][64·2·9·Cin] + the fold's block sums
+    const int rows = 4 * smallcin_wgrad_grid(d, nullptr);
+    return (size_t)(rows + cdiv(rows, SCF_R)) * 64 * (2 * 9 * d->Cin) * sizeof(float);
+  }
   return (size_t)smallcin_rows((long long)d->N * d->H * d->W) * d->Cout * d->Cin * 9 * sizeof(float);
 }
 
@@ -669,9 +684,18 @@ int smallcin_wgrad(const unet_wgrad_desc* d, hipStream_t st) {
       hipLaunchKernelGGL(smallcin_wgrad_mfma_kernel<f16>, dim3(grid), dim3(256), 0, st, *d, t, part);
     int e = check_launch("smallcin_wgrad_mfma");
     if (e) return e;
-    if (d->Cin == 1) hipLaunchKernelGGL(smallcin_fold_kernel<9>, dim3(64), dim3(256), 0, st, part, 4 * grid, 64, d->dw, d->accum);
-    else if (d->Cin == 2) hipLaunchKernelGGL(smallcin_fold_kernel<18>, dim3(64), dim3(256), 0, st, part, 4 * grid, 64, d->dw, d->accum);
-    else hipLaunchKernelGGL(smallcin_fold_kernel<27>, dim3(64), dim3(256), 0, st, part, 4 * grid, 64, d->dw, d->accum);
+    const int rows = 4 * grid, W = 64 * 2 * 9 * d->Cin, nb = cdiv(rows, SCF_R);
+    float* sums = part + (size_t)rows * W;   // after the partial table (smallcin_wgrad_ws)
+    const dim3 g2(cdiv(64 * 9 * d->Cin, 8));
+#define SCF_LAUNCH(CI)                                                                                          \
+  do {                                                                                                        \
+    hipLaunchKernelGGL(smallcin_fold1_kernel<CI>, dim3(nb), dim3(256), 0, st, part, rows, sums);             \
+    hipLaunchKernelGGL(smallcin_fold2_kernel<CI>, g2, dim3(256), 0, st, sums, nb, d->dw, d->accum);          \
+  } while (0)
+    if (d->Cin == 1) SCF_LAUNCH(1);
+    else if (d->Cin == 2) SCF_LAUNCH(2);
+    else SCF_LAUNCH(3);
+#undef SCF_LAUNCH
     return check_launch("smallcin_fold");
   }
   const int rows = smallcin_rows((long long)d->N * d->H * d->W);
