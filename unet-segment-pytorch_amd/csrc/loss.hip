@@ -25,9 +25,11 @@ struct LossSets {
   float w[LMAXS];
 };
 
+// partial rows per image: 1024 pixels each (4 per thread; round 5 — 4096-pixel rows left the bs-4 512^2 reduce
+// on 256 blocks, 16 dependent pixel iterations per thread: 19 us for 16 MB)
 static inline int loss_rows(long long HW) {
-  long long r = (HW + 4095) / 4096;
-  if (r > 256) r = 256;
+  long long r = (HW + 1023) / 1024;
+  if (r > 1024) r = 1024;
   if (r < 1) r = 1;
   return (int)r;
 }
@@ -253,7 +255,8 @@ int unet_loss_finalize_multi(const float* partial, int rows, int S, const float*
   load_sets(S, zs, nullptr, set_weights, ls);
   const size_t shm = (size_t)(N + N * K + N * (4 + 3 * K)) * sizeof(double);
   if (shm > 60000) { set_error("unet_loss_finalize: batch too large"); return UNET_ERR_UNSUPPORTED; }
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), shm, (hipStream_t)stream, partial, rows, S, ls, N, K,
+  // 16 waves: the (image, field) row sums are one memory round trip each, spread over more waves
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), shm, (hipStream_t)stream, partial, rows, S, ls, N, K,
                      ce_w, dice_w, class_w, ce_smooth, dice_smooth, ignore_bg, reduction, loss, coef);
   return check_launch("loss_finalize");
 }
