@@ -7,6 +7,7 @@ missing or no ROCm GPU is visible, every compute entry point raises.
 from __future__ import annotations
 
 import ctypes
+import sys
 import os
 from pathlib import Path
 
@@ -203,8 +204,13 @@ class _GuardedLib:
             guard_check(f"before {name} (a torch op since the previous library call)")
             rc = fn(*args)
             guard_check(name)
+            _GuardedLib.calls += 1
+            if _GuardedLib.calls % 500 == 0:   # a heartbeat: a guarded run is slow (a sync + a band scan per call)
+                print(f"[guard] {_GuardedLib.calls} library calls checked, last {name}", file=sys.__stderr__, flush=True)
             return rc
         return wrapped
+
+    calls = 0
 
 
 if _GUARD:
