@@ -83,6 +83,7 @@ for step in ${STEPS:-tests smoke bench}; do
     grep -v amdgpu.ids $O/guard.log | tail -25 ;;
   faulttrace)  # the round-4 fault test once, bounds-checked (UNET_GUARD=1: our and torch's allocations) under a kernel trace
     UNET_GUARD=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ft -o ft -- python -u -m pytest -x -v -s -p no:cacheprovider tests/test_gpu_parity.py::test_fp16_grad_scaler_steps > $O/faulttrace.log 2>&1 || fail faulttrace $O/faulttrace.log 40
+    find $O/ft -name "*kernel_trace.csv" -delete   # keep the stats (the per-dispatch trace of a guarded run is > 64 MiB)
     grep -E "passed|failed|Guard" $O/faulttrace.log | tail -3 ;;
   gdiag)
     timeout -k 10 180 python -u tools/graphed_diag.py > $O/graphed_diag.log 2>&1 || fail gdiag $O/graphed_diag.log 40
