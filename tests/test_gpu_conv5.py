@@ -215,7 +215,8 @@ def test_conv5_splitk_y_stats(prec, src, shape, mi2, monkeypatch):
     assert ((sm[1] - (r * r).sum(0)).abs() <= 1e-2 * (r * r).sum(0) + 1e-2).all()
 
 
-SPLIT_DGRAD_SHAPES = [(4, 32, 32, 512, 512), (4, 32, 32, 256, 512), (2, 16, 16, 256, 128), (2, 16, 24, 64, 64)]
+SPLIT_DGRAD_SHAPES = [(4, 32, 32, 512, 512), (4, 32, 32, 256, 512), (2, 16, 16, 256, 128), (2, 16, 24, 64, 64),
+                      (4, 64, 64, 256, 512)]   # the last: MI = 2 without split-K (the network's 64^2 512 -> 256 dgrad form)
 
 
 @pytest.mark.parametrize("mi2", ["0", "1"])

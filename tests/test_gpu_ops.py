@@ -719,7 +719,8 @@ def test_wgrad_source_kinds(prec, shape, kind):
 @pytest.mark.parametrize("regime", ["centered", "offset"])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 @pytest.mark.parametrize("shape", [(4, 256, 256, 64, 64), (4, 128, 128, 128, 128), (2, 64, 64, 256, 256),
-                                   (1, 24, 40, 64, 64), (2, 20, 36, 36, 20), (3, 33, 20, 96, 128)],
+                                   (1, 24, 40, 64, 64), (2, 20, 36, 36, 20), (3, 33, 20, 96, 128),
+                                   (4, 64, 64, 256, 128)],   # conv5's MI = 2 form without split-K
                          ids=lambda s: "x".join(map(str, s)))
 def test_dgrad_y_bn_backward_sums(prec, shape, regime, path, monkeypatch):
     """The dgrad y epilogue's fused BatchNorm-backward reduction (unet_conv_desc.bnb_*): per channel
