@@ -433,8 +433,14 @@ static W5Plan wgrad5_plan(const unet_wgrad_desc* d) {
   if ((double)d->N * d->H * d->W * d->Cout * 2 >= (double)OOB) p.ok = false;
   if ((double)d->N * d->H * d->W * 4 >= (double)OOB) p.ok = false;
   if (!p.ok) return p;
-  p.wco = d->Cout >= 128 ? 2 : 1;
-  p.wk = d->Cout >= 128 ? 1 : 2;
+  // 64-output-channel blocks everywhere (round 5): twice the channel tiles of the former 128-channel blocks for
+  // Cout >= 128, so half the splits — and half the fp32 slab traffic (every split writes a whole weight-sized
+  // slab that the reduction reads back): 10-15 % per layer, 73-120 us per step (profiles/r05_wgrad5_wco_ab.txt).
+  // UNET_W5_WCO2=1: the 128-channel blocks for Cout >= 128 (A/B)
+  const char* wco2 = getenv("UNET_W5_WCO2");
+  const bool wide = wco2 && atoi(wco2) && d->Cout >= 128;
+  p.wco = wide ? 2 : 1;
+  p.wk = wide ? 1 : 2;
   const int bco = 64 * p.wco, bci = 64;
   // 4-row stages where the LDS allows (stored sources, 64-channel output blocks): the halo rows cost 6/4
   // instead of 4/2 of a stage's rows and each wave runs two K steps per stage
