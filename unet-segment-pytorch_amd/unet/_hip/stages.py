@@ -798,9 +798,19 @@ class NetworkPlan:
         self.with_ds = self.ds and training
         self._bwd_packed = False
         cbs = self.convbns()
-        for cb, wp in zip(cbs, pack_many([(cb.conv.weight, False) for cb in cbs], prec)):
+        jobs = [(cb.conv.weight, False) for cb in cbs]
+        # a training forward that a backward follows also packs the transposed (dgrad) weights, in the same
+        # launch: the fp32 weights are read once (the second layout from cache) and the backward has no pack
+        # launch of its own (round 5; prepare_backward still packs them when this did not)
+        tcbs = [cb for cb in cbs if cb is not self.inc.c1 or need_dx] if (tracked and training) else []
+        jobs += [(cb.conv.weight, True) for cb in tcbs]
+        packed = pack_many(jobs, prec)
+        for cb, wp in zip(cbs, packed[:len(cbs)]):
             cb.pre_wp = wp
             cb.tracked = tracked
+        for cb, wt in zip(tcbs, packed[len(cbs):]):
+            cb.pre_wt = wt
+        self._bwd_packed = bool(tcbs)
         self.xs, self.dec = [], []
 
     def fwd_inc(self):
