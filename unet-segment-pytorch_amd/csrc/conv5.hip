@@ -428,9 +428,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   };
   // this wave's DMAs of the chunk after K have landed: only the youngest chunk's may still be in flight
   // (the y epilogue's NST stores sit between DMA batches for the two chunks after it: sw counts them down)
-  // (BNB: the epilogue's 4 MI 8-byte g stores likewise; and the tile's NYL y1 loads, issued at the start of
+  // (BNB: the epilogue's 2 MI 16-byte g stores likewise; and the tile's NYL y1 loads, issued at the start of
   // its last chunk — after the two in-flight DMA batches — are counted by that chunk's wait: yl)
-  constexpr int NST = NJ * (OM == OM5_Y ? 2 * MI : (OM == OM5_BNB || OM == OM5_F32 ? 4 * MI : 0));
+  constexpr int NST = NJ * (OM == OM5_Y || OM == OM5_BNB ? 2 * MI : (OM == OM5_F32 ? 4 * MI : 0));
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
   // F32 without accumulation: counted buffer stores (no RMW loads, whose compiler waits drain the DMA queue)
   const bool f32_counted = OM == OM5_F32 && !d.accum && !d.accum2 && (d.split % 8) == 0 &&
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   const rsrc_t rf1 = mk_rsrc(SPLIT ? (const void*)((const char*)d.out + (size_t)blockIdx.z * (size_t)npix * d.Cout * 4) : d.out,
                              (unsigned)(f32_counted ? npix * d.split * 4 : 0));
   const rsrc_t rf2 = mk_rsrc(d.out2 ? d.out2 : d.out, (unsigned)(f32_counted ? npix * (d.Cout - d.split) * 4 : 0));
-  constexpr int NYL = OM == OM5_BNB ? 4 * MI * NJ : 0;
+  constexpr int NYL = OM == OM5_BNB ? 2 * MI * NJ : 0;
   int sw = 0;
   auto wait_next = [&](bool yl) {
     const bool st = NST && sw > 0;
@@ -492,8 +492,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   if constexpr (PIPE) load_col(K, 0, xA, wA);
   // BNB: the activation y1 of this wave's tile pixels (buffer loads, out-of-range offsets for masked lanes:
   // a fixed count), loaded during the tile's last chunk so that the epilogue's wait for them does not drain
-  // the next chunks' DMAs (their issue follows the epilogue)
-  uint2 yv[OM == OM5_BNB ? MI : 1][NJ][4];
+  // the next chunks' DMAs (their issue follows the epilogue).  16-byte loads in the layout of the epilogue's
+  // swapped g stores: lanes 0-31 channels 16h+0..7 of their pixel, lanes 32-63 channels 16h+8..15
+  uint4 yv[OM == OM5_BNB ? MI : 1][NJ][2];
   const rsrc_t ry1 = mk_rsrc(OM == OM5_BNB ? d.bnb_y : d.out, (unsigned)(npix * d.Cout * 2));
   auto load_y1 = [&](const Cur& q) {   // K's tile (its last chunk)
     const int n = q.n, h0 = q.h0, w0 = q.w0;
@@ -504,11 +505,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int co = cw0 + 32 * j + 8 * gq + 4 * (lane >> 5);
+        for (int h = 0; h < 2; ++h) {
+          const int co = cw0 + 32 * j + 16 * h + 8 * (lane >> 5);
           const bool ok = ow < d.W && oh0 + i < d.H && co < d.Cout;
           const unsigned vo = ok ? ((pix0 + (unsigned)i * d.W) * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
-          yv[i][j][gq] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ry1, (int)vo, 0, 0));
+          yv[i][j][h] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ry1, (int)vo, 0, 0));
         }
   };
   for (int ti = 0; ti < ntl; ++ti) {
@@ -637,35 +638,48 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
       // block's channels from the LDS table the prologue filled; y1 from the loads of the last chunk
       const float* btab = reinterpret_cast<const float*>(lds + Lay::OFF_BTAB);
       const rsrc_t rg = mk_rsrc(d.out, (unsigned)(npix * d.Cout * 2));
+      // g packed and v_permlane32_swap'ed as the y epilogue (one 16-byte store per 8 channels): this lane then
+      // holds channels co..co+7 (co = cw0 + 32j + 16h + 8hh) of its pixel — sum slot 8h + r is channel co + r
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int co = cw0 + 32 * j + 8 * gq + 4 * hh;
+      for (int h = 0; h < 2; ++h) {
+        const int co = cw0 + 32 * j + 16 * h + 8 * hh;
         const bool cok = co < d.Cout;
         const int cb = co - (int)blockIdx.y * C5_BN;
-        const float4 a4 = *reinterpret_cast<const float4*>(btab + cb);
-        const float4 b4 = *reinterpret_cast<const float4*>(btab + C5_BN + cb);
-        const float sc4[4] = {a4.x, a4.y, a4.z, a4.w}, sf4[4] = {b4.x, b4.y, b4.z, b4.w};
+        float sc8[8], sf8[8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float4 a4 = *reinterpret_cast<const float4*>(btab + cb + 4 * q);
+          const float4 b4 = *reinterpret_cast<const float4*>(btab + C5_BN + cb + 4 * q);
+          sc8[4 * q] = a4.x; sc8[4 * q + 1] = a4.y; sc8[4 * q + 2] = a4.z; sc8[4 * q + 3] = a4.w;
+          sf8[4 * q] = b4.x; sf8[4 * q + 1] = b4.y; sf8[4 * q + 2] = b4.z; sf8[4 * q + 3] = b4.w;
+        }
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const unsigned pix = pix0 + (unsigned)i * d.W;
           const bool ok = colok && i < rows && cok;
-          uint2 pk;
-          pk.x = pack2_16<T>(acc[i][j][4 * gq], acc[i][j][4 * gq + 1]);
-          pk.y = pack2_16<T>(acc[i][j][4 * gq + 2], acc[i][j][4 * gq + 3]);
+          const int g0 = 2 * h;
+          const unsigned pxa = pack2_16<T>(acc[i][j][4 * g0], acc[i][j][4 * g0 + 1]);
+          const unsigned pxb = pack2_16<T>(acc[i][j][4 * g0 + 4], acc[i][j][4 * g0 + 5]);
+          const unsigned pya = pack2_16<T>(acc[i][j][4 * g0 + 2], acc[i][j][4 * g0 + 3]);
+          const unsigned pyb = pack2_16<T>(acc[i][j][4 * g0 + 6], acc[i][j][4 * g0 + 7]);
+          const auto sx = __builtin_amdgcn_permlane32_swap(pxa, pxb, false, false);
+          const auto sy = __builtin_amdgcn_permlane32_swap(pya, pyb, false, false);
           const unsigned vo = ok ? (pix * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
-          typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), rg, (int)vo, 0, 0);
+          const u32x4_t v4 = {sx[0], sy[0], sx[1], sy[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(v4, rg, (int)vo, 0, 0);
           if (ok) {
-            float gv[4], yy[4];
-            unpack4_16<T>(pk, gv);
-            unpack4_16<T>(yv[i][j][gq], yy);
+            float gv[8], yy[8];
+            unpack4_16<T>(make_uint2(v4[0], v4[1]), gv);
+            unpack4_16<T>(make_uint2(v4[2], v4[3]), gv + 4);
+            unpack4_16<T>(make_uint2(yv[i][j][h].x, yv[i][j][h].y), yy);
+            unpack4_16<T>(make_uint2(yv[i][j][h].z, yv[i][j][h].w), yy + 4);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float gg = (d.bnb_relu && !(yy[r] * sc4[r] + sf4[r] > 0.f)) ? 0.f : gv[r];
-              sA[j][4 * gq + r] += gg;
-              sB[j][4 * gq + r] = __builtin_fmaf(gg, yy[r], sB[j][4 * gq + r]);
+            for (int r = 0; r < 8; ++r) {
+              const float gg = (d.bnb_relu && !(yy[r] * sc8[r] + sf8[r] > 0.f)) ? 0.f : gv[r];
+              sA[j][8 * h + r] += gg;
+              sB[j][8 * h + r] = __builtin_fmaf(gg, yy[r], sB[j][8 * h + r]);
             }
           }
         }
@@ -753,8 +767,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int co = cw0 + 32 * j + 8 * gq + 4 * hh;
+      for (int gq = 0; gq < 4; ++gq) {   // slot 8h + r: channel cw0 + 32j + 16h + 8hh + r (the BNB epilogue)
+        const int co = cw0 + 32 * j + 16 * (gq >> 1) + 8 * hh + 4 * (gq & 1);
         float a[4], b[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
