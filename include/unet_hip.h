@@ -26,6 +26,10 @@
 extern "C" {
 #endif
 
+/* unet_version() of a library built from this header.  110: unet_conv_desc gained `workspace` (round 5);
+ * a caller built against an older header must not pass its (shorter) descriptors to this library */
+#define UNET_ABI_VERSION 110
+
 enum { UNET_F32 = 0, UNET_BF16 = 1, UNET_F16 = 2 };  /* operand (activation / weight) type */
 enum { UNET_ERR_ARG = 1001, UNET_ERR_UNSUPPORTED = 1002 };
 
@@ -110,8 +114,10 @@ typedef struct unet_conv_desc {
    * attention gate, layers.py:33-34,192), op dtype [N,H,W,src[0].C], written once — the weight
    * gradient of this conv then reads a stored map instead of re-applying the transform               */
   void* act_out;
-  /* scratch of unet_conv_workspace(d) bytes (device), or NULL when that is 0: the split-K form of the 3x3
-   * conv on maps too small to fill the chip keeps its fp32 partial sums there                        */
+  /* scratch of unet_conv_workspace(d) bytes (device), or NULL: the split-K form of the 3x3 conv on maps
+   * too small to fill the chip keeps its fp32 partial sums there.  Optional: with NULL, unet_conv runs
+   * the unsplit form (slower on those maps, same contract).  unet_conv_stats_rows depends on it: ask
+   * with the workspace pointer you will launch with                                                   */
   void* workspace;
 } unet_conv_desc;
 
@@ -127,14 +133,15 @@ typedef struct unet_wgrad_desc {
 
 /* ---- misc ---------------------------------------------------------------------------------- */
 const char* unet_last_error(void);
-int unet_version(void);
+int unet_version(void);   /* == UNET_ABI_VERSION */
 /* number of M tiles (8x16 output pixels) of a conv with this geometry: rows of the stats buffer  */
 int unet_conv_mtiles(int N, int H, int W);
 /* rows of the BN partial-sum buffer (stats = float[2][Cout][rows]) unet_conv will write for d    */
 int unet_conv_stats_rows(const unet_conv_desc* d);
 /* name of the kernel instantiation unet_conv dispatches d to (for profiling / roofline probes)   */
 int unet_conv_variant(const unet_conv_desc* d, char* buf, int len);
-/* bytes of d->workspace unet_conv needs for d (0: none)                                           */
+/* bytes of d->workspace the split-K form of d needs (0: d has no split-K form); independent of
+ * d->workspace itself                                                                             */
 size_t unet_conv_workspace(const unet_conv_desc* d);
 /* does unet_conv write d->act_out for this descriptor (else the caller keeps the activation source)? */
 int unet_conv_act_out_ok(const unet_conv_desc* d);

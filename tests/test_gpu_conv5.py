@@ -71,6 +71,7 @@ def test_conv5_y_stats(prec, src, shape, path):
     d0.dtype, d0.N, d0.H, d0.W, d0.Cin, d0.Cout, d0.ksize, d0.nsrc = R._PRECISIONS[prec].code, N, H, W, cin, cout, 3, len(srcs)
     for i, s in enumerate(srcs):
         d0.src[i] = s
+    ws0 = L.attach_workspace(d0, "cuda")   # (the split-K forms' row count: ask with a workspace, as _conv launches)
     rows = L.load().unet_conv_stats_rows(d0)
     st = torch.full((2, cout, rows), float("nan"), device="cuda")
     out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
@@ -195,6 +196,7 @@ def test_conv5_splitk_y_stats(prec, src, shape, mi2, monkeypatch):
     d0.dtype, d0.N, d0.H, d0.W, d0.Cin, d0.Cout, d0.ksize, d0.nsrc = R._PRECISIONS[prec].code, N, H, W, cin, cout, 3, len(srcs)
     for i, s in enumerate(srcs):
         d0.src[i] = s
+    ws0 = L.attach_workspace(d0, "cuda")   # (the split-K forms' row count: ask with a workspace, as _conv launches)
     rows = L.load().unet_conv_stats_rows(d0)
     outs = []
     for _ in range(2):
@@ -213,6 +215,40 @@ def test_conv5_splitk_y_stats(prec, src, shape, mi2, monkeypatch):
     assert torch.isfinite(sm).all()
     assert ((sm[0] - r.sum(0)).abs() <= 1e-3 * r.abs().sum(0) + 1e-2).all()
     assert ((sm[1] - (r * r).sum(0)).abs() <= 1e-2 * (r * r).sum(0) + 1e-2).all()
+
+
+@pytest.mark.parametrize("prec", ["bf16"])
+def test_conv5_small_map_without_workspace(prec, monkeypatch):
+    """a descriptor without a workspace (a zero-initialised C caller) on a split-K shape runs the unsplit
+    form — correct y and BN sums, and unet_conv_stats_rows asked the same way agrees with what the launch writes."""
+    monkeypatch.setenv("UNET_CONV5_MI2", "1")
+    L, R = _lib(), _rt()
+    N, H, W, cin, cout = 4, 32, 32, 512, 512
+    dt = DT[prec]
+    torch.manual_seed(43)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") * (2.0 / (9 * cin)) ** 0.5).to(dt).float()
+    y = _rand(N, H, W, cin, dt=dt)
+    s = L.Src()
+    s.kind, s.C, s.H, s.W, s.data = L.SRC_PLAIN, cin, H, W, y.data_ptr()
+    P = R._PRECISIONS[prec]
+    d = L.ConvDesc()
+    d.dtype, d.N, d.H, d.W, d.Cin, d.Cout, d.ksize, d.nsrc = P.code, N, H, W, cin, cout, 3, 1
+    d.src[0] = s
+    assert L.load().unet_conv_workspace(d) > 0          # the shape has a split-K form
+    wp = R.pack_weight(w, P, transpose=False)
+    rows = L.load().unet_conv_stats_rows(d)
+    st = torch.full((2, cout, rows), float("nan"), device="cuda")
+    out = torch.full((N, H, W, cout), float("nan"), dtype=dt, device="cuda")
+    d.weight, d.out_mode, d.out, d.stats = wp.data_ptr(), L.OUT_Y, out.data_ptr(), st.data_ptr()
+    assert "splitk" not in _variant(d), _variant(d)
+    L.call("unet_conv", d, R.stream())
+    torch.cuda.synchronize()
+    ref = F.conv2d(y.float().permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
+    _close_bf16(out.float(), ref, "y")
+    r = ref.double().reshape(-1, cout)
+    sm = st.double().sum(-1)
+    assert torch.isfinite(sm).all()
+    assert ((sm[0] - r.sum(0)).abs() <= 1e-3 * r.abs().sum(0) + 1e-2).all()
 
 
 SPLIT_DGRAD_SHAPES = [(4, 32, 32, 512, 512), (4, 32, 32, 256, 512), (2, 16, 16, 256, 128), (2, 16, 24, 64, 64),

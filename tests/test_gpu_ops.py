@@ -61,8 +61,10 @@ def _conv(prec, srcs, N, H, W, cin, w, k, out_mode, **kw):
     d.out_mode = out_mode
     for key, v in kw.items():
         setattr(d, key, v)
+    ws = L.attach_workspace(d, "cuda")   # the split-K form where d has one (kept set on d: the row queries)
     L.call("unet_conv", d, R.stream())
     torch.cuda.synchronize()
+    del ws
     return d
 
 
@@ -524,6 +526,7 @@ def test_conv3_bench_tiles_y(prec, shape, stats, monkeypatch):
         d0 = L.ConvDesc()
         d0.dtype, d0.N, d0.H, d0.W, d0.Cin, d0.Cout, d0.ksize, d0.nsrc = _rt()._PRECISIONS[prec].code, N, H, W, cin, cout, 3, 1
         d0.src[0] = _act_src(y, ab)
+        ws0 = L.attach_workspace(d0, "cuda")
         rows = L.load().unet_conv_stats_rows(d0)
         st = torch.empty(2, cout, rows, device="cuda")
         kw["stats"] = st.data_ptr()
@@ -761,6 +764,7 @@ def test_dgrad_y_bn_backward_sums(prec, shape, regime, path, monkeypatch):
     d.out = g.data_ptr()
     d.bnb_y, d.bnb_scale, d.bnb_shift, d.bnb_relu = y1.data_ptr(), ab[0].data_ptr(), ab[1].data_ptr(), 1
     d.bnb_mean, d.bnb_invstd = mean.data_ptr(), invstd.data_ptr()
+    ws = L.attach_workspace(d, "cuda")
     rows = L.load().unet_conv_stats_rows(d)
     part = torch.full((2, rows, cmid), float("nan"), device="cuda")
     d.bnb_stats = part.data_ptr()

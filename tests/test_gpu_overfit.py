@@ -22,8 +22,10 @@ reference's own measured spread:
     hence the same Tumor-Dice, and one training step from each state has the reference's loss and gradients no
     further from fp64 than the reference's own fp32 step (3x + 1e-5);
   * test_overfit_c1_tumor_dice_vs_reference_spread: the first 16 epochs step for step;
-  * test_overfit_c1_full_protocol_final_dice: 200 epochs; the last-epoch Tumor-Dice within
-    max(1e-3, max_k |ref32_k - ref64|) of the fp64 oracle's, the bound measured in the same test."""
+  * test_overfit_c1_full_protocol_final_dice: 200 epochs from the seeded weights; the last-epoch Tumor-Dice
+    within max(1e-3, min(5e-3, |ref32_0 - ref64_0|)) of the fp64 oracle started from the same weights;
+  * test_overfit_c1_ensemble_vs_reference: 8 same-start members each of HIP and the reference fp32 (one-ulp
+    perturbations): medians within max(1e-3, the reference's IQR), and HIP collapses no more often."""
 
 import contextlib
 import sys
@@ -75,18 +77,26 @@ def test_overfit_c1_tumor_dice_vs_reference_spread(c1):
     assert hip[-1][1] > 0.8 and r32[-1][1] > 0.8 and r64[-1][1] > 0.8
 
 
+K_ENS = 8          # same-start members of the ensemble gate (>= 8 seeds)
+COLLAPSE = 0.99    # a member "collapsed" when its mean Tumor-Dice over the last 10 epochs is below this
+BOUND_CAP = 5e-3   # the member-0 bound's self-calibrated part is capped: never looser than this
+
+
 @pytest.fixture(scope="module")
 def c1_full(c1, request):
     D, init, names, x, t = c1
-    # five 200-epoch executions (minutes): with pytest's output capture suspended, so their progress lines
+    # K_ENS 200-epoch executions each of HIP and of the reference fp32, member k started from the seeded weights
+    # perturbed by one ulp in a random half of their elements (member 0: unperturbed), plus the reference fp64
+    # from member 0's start (minutes): with pytest's output capture suspended, so their progress lines
     # (tools/overfit_diag.py) reach the runner's log while they run
     cm = request.config.pluginmanager.getplugin("capturemanager")
     with cm.global_and_fixture_disabled() if cm is not None else contextlib.nullcontext():
-        hip = D.run_hip(init, x, t, 200, 64)
-        r32, snaps = D.run_oracle(init, names, x, t, 200, torch.float32, snap=set(PINS))
-        r32p = [D.run_oracle(D.perturb(init, names, s), names, x, t, 200, torch.float32) for s in (1, 2)]
+        hip = [D.run_hip(D.perturb(init, names, k), x, t, 200, 64) for k in range(K_ENS)]
+        r32_0, snaps = D.run_oracle(init, names, x, t, 200, torch.float32, snap=set(PINS))
+        r32 = [r32_0] + [D.run_oracle(D.perturb(init, names, k), names, x, t, 200, torch.float32)
+                         for k in range(1, K_ENS)]
         r64 = D.run_oracle(init, names, x, t, 200, torch.float64)
-    return hip, [r32] + r32p, r64, snaps
+    return hip, r32, r64, snaps
 
 
 def test_overfit_c1_eval_and_step_pins(c1, c1_full):
@@ -108,19 +118,55 @@ def test_overfit_c1_eval_and_step_pins(c1, c1_full):
         assert bh <= 3.0 * b32 + 1e-7, (e, bh, b32)
 
 
+def _median(v):
+    v = sorted(v)
+    n = len(v)
+    return v[n // 2] if n % 2 else 0.5 * (v[n // 2 - 1] + v[n // 2])
+
+
+def _iqr(v):
+    q = torch.quantile(torch.tensor(v, dtype=torch.float64), torch.tensor([0.25, 0.75], dtype=torch.float64))
+    return float(q[1] - q[0])
+
+
 def test_overfit_c1_full_protocol_final_dice(c1, c1_full):
     """The reference's whole protocol (200 epochs, overfit_test.py:69) and its statistic, the last epoch's
-    Tumor-Dice (overfit_test.py:218,288): within max(1e-3, S) of the fp64 oracle's, S = the largest
-    |ref32_k - ref64| over the reference's fp32 executions (seeded + two one-ulp perturbations) in this test."""
-    hip, refs, r64, _ = c1_full
-    print("\nlast 10 epochs: dice_hip dice_ref64 | dice_ref32 (seeded, perturbed 1, perturbed 2)")
+    Tumor-Dice (overfit_test.py:218,288), from the seeded weights (member 0): HIP within max(1e-3, S) of the fp64
+    oracle started from the SAME weights, S = |ref32_0 - ref64_0| (the reference's own fp32-vs-fp64 difference on
+    that start) capped at BOUND_CAP."""
+    hip, r32, r64, _ = c1_full
+    print("\nlast 10 epochs of member 0: dice_hip dice_ref32 dice_ref64")
     for i in range(190, 200):
-        print(i, "%.6f %.6f |" % (hip[i][1], r64[i][1]), " ".join("%.6f" % r[i][1] for r in refs))
-    last = hip[-1][1]
-    spread = max(abs(r[-1][1] - r64[-1][1]) for r in refs)
-    bound = max(1e-3, spread)
-    print(f"last epoch: HIP {last:.6f}, reference fp64 {r64[-1][1]:.6f}, reference fp32 "
-          f"{' / '.join('%.6f' % r[-1][1] for r in refs)}; |HIP - fp64| {abs(last - r64[-1][1]):.2e}, "
-          f"bound max(1e-3, fp32 spread {spread:.2e}) = {bound:.2e}")
+        print(i, "%.6f %.6f %.6f" % (hip[0][i][1], r32[0][i][1], r64[i][1]))
+    last = hip[0][-1][1]
+    spread = abs(r32[0][-1][1] - r64[-1][1])
+    bound = max(1e-3, min(BOUND_CAP, spread))
+    print(f"member 0 last epoch: HIP {last:.6f}, reference fp32 {r32[0][-1][1]:.6f}, fp64 {r64[-1][1]:.6f}; "
+          f"|HIP - fp64| {abs(last - r64[-1][1]):.2e}, bound max(1e-3, min({BOUND_CAP:g}, |fp32 - fp64| {spread:.2e}))"
+          f" = {bound:.2e} (north_star: 1e-3)")
     assert abs(last - r64[-1][1]) <= bound, (last, r64[-1][1], bound)
-    assert last > 0.8 and r64[-1][1] > 0.8 and all(r[-1][1] > 0.8 for r in refs)   # overfit_test.py:288
+    assert last > 0.8 and r64[-1][1] > 0.8 and r32[0][-1][1] > 0.8   # overfit_test.py:288
+
+
+def test_overfit_c1_ensemble_vs_reference(c1, c1_full):
+    """The statistic's distribution under rounding noise: K_ENS members each of HIP and
+    of the reference fp32, member k of both from the same one-ulp-perturbed start.  (1) |median(HIP) -
+    median(ref32)| of the last-epoch Tumor-Dice <= max(1e-3, the ref32 interquartile range); (2) HIP collapses no
+    more often than the reference: #members whose mean Dice over the last 10 epochs is below COLLAPSE, HIP <=
+    ref32 + 1."""
+    hip, r32, _, _ = c1_full
+    lh = [h[-1][1] for h in hip]
+    l32 = [r[-1][1] for r in r32]
+    mh = [sum(e[1] for e in h[-10:]) / 10 for h in hip]
+    m32 = [sum(e[1] for e in r[-10:]) / 10 for r in r32]
+    print("\nmember: last-epoch dice HIP ref32 | mean of last 10 HIP ref32")
+    for k in range(K_ENS):
+        print(f"{k}: {lh[k]:.6f} {l32[k]:.6f} | {mh[k]:.6f} {m32[k]:.6f}")
+    dmed = abs(_median(lh) - _median(l32))
+    iqr = _iqr(l32)
+    bound = max(1e-3, iqr)
+    ch, c32 = sum(m < COLLAPSE for m in mh), sum(m < COLLAPSE for m in m32)
+    print(f"median last-epoch dice: HIP {_median(lh):.6f}, ref32 {_median(l32):.6f}; |diff| {dmed:.2e}, bound "
+          f"max(1e-3, ref32 IQR {iqr:.2e}) = {bound:.2e}; members with mean-of-last-10 < {COLLAPSE}: HIP {ch}, ref32 {c32}")
+    assert dmed <= bound, (dmed, bound)
+    assert ch <= c32 + 1, (ch, c32)

@@ -83,7 +83,9 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(so, s), s
     assert set(syms) == set(L.exported_symbols()), "lib.py signatures out of sync with the header"
-    assert L.load().unet_version() == 100
+    assert L.load().unet_version() == L.ABI_VERSION
+    hdr = (ROOT / "include" / "unet_hip.h").read_text()
+    assert f"#define UNET_ABI_VERSION {L.ABI_VERSION}" in hdr
 
 
 def test_no_cpu_fallback():

@@ -46,11 +46,11 @@ def layer(N, H, W, cin, cout, kind):
     y = torch.empty(N, H, W, cout, dtype=torch.bfloat16, device=dev)
     d.out_mode = L.OUT_Y
     d.out = y.data_ptr()
+    ws = torch.empty(max(lib.unet_conv_workspace(ctypes.byref(d)), 16), dtype=torch.uint8, device=dev)
+    d.workspace = ws.data_ptr()
     rows = lib.unet_conv_stats_rows(d)
     st = f32(2, cout, rows, device=dev)
     d.stats = st.data_ptr()
-    ws = torch.empty(max(lib.unet_conv_workspace(ctypes.byref(d)), 16), dtype=torch.uint8, device=dev)
-    d.workspace = ws.data_ptr()
     return d, (x, w, wp, ab, y, st, ws)
 
 

@@ -17,5 +17,5 @@ int check_launch(const char* what) {
 
 extern "C" {
 const char* unet_last_error(void) { return unet::g_err; }
-int unet_version(void) { return 100; }
+int unet_version(void) { return UNET_ABI_VERSION; }
 }

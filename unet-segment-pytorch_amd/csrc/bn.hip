@@ -97,8 +97,19 @@ __device__ __forceinline__ void bn_finalize_body(const float* stats, int rows, i
       rmean[c] = (float)((1.0 - f) * (double)rm_ + f * m);
       rvar[c] = (float)((1.0 - f) * (double)rv_ + f * unb);
     }
-    if (c == 0 && nbt) *nbt += 1;
+    // momentum=None reads *nbt in every block, so block 0 must not increment it in the same launch (a block
+    // scheduled after it would use 1/(nbt+2)): that case increments in a follow-up launch (bn_nbt_inc_kernel)
+    if (c == 0 && nbt && momentum >= 0) *nbt += 1;
   }
+}
+
+// ++num_batches_tracked of the momentum=None finalizes, after every block of the finalize has read the old value
+struct BnNbtList {
+  long long* p[UNET_BN_MULTI_MAX];
+  int n;
+};
+__global__ void bn_nbt_inc_kernel(const BnNbtList l) {
+  if (threadIdx.x < (unsigned)l.n) *l.p[threadIdx.x] += 1;
 }
 
 __global__ void bn_finalize_kernel(const float* stats, int rows, int C, long long count, const float* gamma,
@@ -537,7 +548,15 @@ int unet_bn_finalize(const float* stats, int rows, int C, long long count, const
   }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(fin_threads(rows)), 0, (hipStream_t)stream, stats, rows, C, count, gamma,
                      beta, running_mean, running_var, nbt, momentum, eps, mean, invstd, scale, shift);
-  return check_launch("bn_finalize");
+  if (int e = check_launch("bn_finalize")) return e;
+  if (nbt && momentum < 0) {
+    BnNbtList l{};
+    l.p[0] = nbt;
+    l.n = 1;
+    hipLaunchKernelGGL(bn_nbt_inc_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, l);
+    return check_launch("bn_finalize nbt");
+  }
+  return 0;
 }
 
 int unet_bn_finalize_multi(int count, const unet_bn_finalize_job* jobs, void* stream) {
@@ -561,7 +580,17 @@ int unet_bn_finalize_multi(int count, const unet_bn_finalize_job* jobs, void* st
     rows_max = j.rows > rows_max ? j.rows : rows_max;
   }
   hipLaunchKernelGGL(bn_finalize_multi_kernel, dim3(js.c0[count]), dim3(fin_threads(rows_max)), 0, (hipStream_t)stream, js);
-  return check_launch("bn_finalize_multi");
+  if (int e = check_launch("bn_finalize_multi")) return e;
+  BnNbtList l{};
+  for (int k = 0; k < count; ++k) {
+    const unet_bn_finalize_job& j = jobs[k];
+    if (j.num_batches_tracked && j.momentum < 0) l.p[l.n++] = j.num_batches_tracked;
+  }
+  if (l.n) {
+    hipLaunchKernelGGL(bn_nbt_inc_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, l);
+    return check_launch("bn_finalize_multi nbt");
+  }
+  return 0;
 }
 
 int unet_bn_bwd_finalize_multi(int count, const unet_bn_bwd_finalize_job* jobs, void* stream) {

@@ -706,7 +706,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
         }
       }
       sw = 2;
-    } else {  // OM5_F32 with read-modify-write (accumulating into an existing gradient)
+    } else if constexpr (!SPLIT) {  // OM5_F32 with read-modify-write (accumulating into an existing gradient;
+      // never a split-K slab: launch5_split_mi's descriptors always take the counted stores above)
       float* o1 = (float*)d.out;
       float* o2 = (float*)d.out2;
       const int c2 = d.Cout - d.split;
@@ -936,6 +937,7 @@ static long long conv5_mtiles(const unet_conv_desc* d, int mi) {
 static int conv5_mi(const unet_conv_desc* d) {
   const char* e = getenv("UNET_CONV5_MI2");   // read per call
   if (e && !atoi(e)) return C5_MI;
+  if (e && atoi(e) == 2) return C5_MI_S;      // (diagnostic: 8-row tiles everywhere)
   return conv5_mtiles(d, C5_MI) * cdiv(d->Cout, C5_BN) >= 256 ? C5_MI : C5_MI_S;
 }
 
@@ -992,11 +994,14 @@ bool conv5_eligible(const unet_conv_desc* d) {
 // S fp32 slabs in d->workspace and conv5_splitk_finish_kernel adds them in slab order (deterministic) and applies
 // the real epilogue (y + BN partial sums, y + BN-backward sums, or fp32 with split / accumulation).
 // UNET_CONV5_SPLIT=0 turns it off (A/B).
-int conv5_splitk(const unet_conv_desc* d) {
+// the split count of d's shape (unet_conv_workspace sizes the slabs from it, whatever d->workspace holds)
+static int conv5_splitk_shape(const unet_conv_desc* d) {
   const char* e = getenv("UNET_CONV5_SPLIT");   // read per call (tests flip it)
   const int on = e ? atoi(e) : 1;
   if (!on || conv5_mode() == 0 || d->act_out || !conv5_shape_ok(d)) return 1;
   if (d->Cout > 1024 || (d->Cout & (d->Cout - 1))) return 1;     // the finisher's channel-vector layout
+  // a slab is addressed by one buffer resource (32-bit range): the kernel's counted fp32 stores need it
+  if ((double)d->N * d->H * d->W * d->Cout * 4 >= (double)OOB) return 1;
   const long long work = conv5_mtiles(d, conv5_mi(d)) * cdiv(d->Cout, C5_BN);
   if (work >= 256) return 1;
   const int nch = cdiv(d->Cin, 16);
@@ -1005,10 +1010,14 @@ int conv5_splitk(const unet_conv_desc* d) {
   return S;
 }
 
+// the split count unet_conv runs d with: the shape's, if the caller passed a workspace (a
+// descriptor without one — e.g. zero-initialised by a C caller — runs the unsplit form, as before round 5)
+int conv5_splitk(const unet_conv_desc* d) { return d->workspace ? conv5_splitk_shape(d) : 1; }
+
 bool conv5_serves(const unet_conv_desc* d) { return conv5_eligible(d) || conv5_splitk(d) > 1; }
 
 size_t conv5_workspace(const unet_conv_desc* d) {
-  const int S = conv5_eligible(d) ? 1 : conv5_splitk(d);
+  const int S = conv5_eligible(d) ? 1 : conv5_splitk_shape(d);
   return S > 1 ? (size_t)S * d->N * d->H * d->W * d->Cout * sizeof(float) : 0;
 }
 
@@ -1089,8 +1098,8 @@ static int launch5_finish(const unet_conv_desc* d, int S, hipStream_t st) {
 template <typename T, int SK, int GATE, int MI>
 static int launch5_split_mi(const unet_conv_desc* d, int S, hipStream_t st) {
   constexpr int TH = C5_WM * MI;
-  if (!d->workspace) {
-    set_error("unet_conv: this descriptor runs split-K and needs d->workspace (unet_conv_workspace bytes)");
+  if (!d->workspace || S < 2 || (double)d->N * d->H * d->W * d->Cout * 4 >= (double)OOB) {   // (conv5_splitk)
+    set_error("unet_conv: split-K without a workspace or past a slab's 32-bit range");
     return UNET_ERR_ARG;
   }
   const int tw = cdiv(d->W, C5_W), th = cdiv(d->H, TH);

@@ -148,6 +148,7 @@ _SIGS = {
 }
 
 _lib = None
+ABI_VERSION = 110   # include/unet_hip.h UNET_ABI_VERSION
 
 # UNET_GUARD=1: bounds-checking debug mode (csrc/guard_alloc.cpp).  Every device allocation of the process
 # gets guard bands and every library call is bracketed by a device sync + a check of all bands, so an
@@ -234,6 +235,9 @@ def load(require_gpu: bool = False):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.unet_version() != ABI_VERSION:   # descriptor layouts below are this version's
+            raise HipLibraryError(f"{_LIB_PATH} has ABI {lib.unet_version()}, this package binds {ABI_VERSION}: "
+                                  "rebuild it (make -C unet-segment-pytorch_amd/csrc)")
         _lib = _GuardedLib(lib) if _GUARD else lib
     if require_gpu and not torch.cuda.is_available():
         raise HipLibraryError("unet HIP path needs a ROCm GPU (MI355X / gfx950); none is visible.")
@@ -250,21 +254,20 @@ def check(rc: int, what: str):
         raise RuntimeError(f"{what} failed (code {rc}): {msg}")
 
 
+def attach_workspace(d, device) -> "torch.Tensor | None":
+    """Give a conv descriptor the scratch of its split-K form (unet_conv_workspace bytes) on `device` — the
+    device of the descriptor's tensors — and return it (the caller keeps it alive while d is launched).  Set
+    it after the descriptor's other fields and BEFORE asking unet_conv_stats_rows: the row count of the split
+    form differs.  Without a workspace unet_conv runs the unsplit form."""
+    n = load().unet_conv_workspace(d)
+    if not n:
+        return None
+    ws = torch.empty(n, dtype=torch.uint8, device=device)
+    d.workspace = ws.data_ptr()
+    return ws
+
+
 def call(name: str, *args):
-    lib = load()
-    if name == "unet_conv" and not args[0].workspace:
-        # the split-K form of a small-map 3x3 conv needs scratch for its fp32 partial sums: allocated here from
-        # torch's caching allocator on the current stream (valid for the kernels enqueued below)
-        n = lib.unet_conv_workspace(args[0])
-        if n:
-            ws = torch.empty(n, dtype=torch.uint8, device="cuda")
-            args[0].workspace = ws.data_ptr()
-            try:
-                rc = lib.unet_conv(*args)
-            finally:
-                args[0].workspace = None
-            check(rc, name)
-            return rc
-    rc = getattr(lib, name)(*args)
+    rc = getattr(load(), name)(*args)
     check(rc, name)
     return rc

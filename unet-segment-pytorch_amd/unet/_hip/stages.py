@@ -117,6 +117,7 @@ class ConvBN:
             d.act_out = act.data_ptr()
             self.wsrcs = [_plain_src(act)] + list(srcs[1:])
             self.wact = act              # the descriptors hold raw pointers: keep the tensor alive
+        ws = L.attach_workspace(d, dev)   # (split-K scratch, before the stats-row query: the row count depends on it)
         bn = self.bn
         ab = f32(2, self.cout, device=dev)
         use_batch = training or not bn.track_running_stats
@@ -250,6 +251,7 @@ class ConvBN:
         wt = self.pre_wt if self.pre_wt is not None else pack_weight(self.conv.weight, prec, transpose=True)
         self.pre_wt = None
         d = _conv_desc(prec, N, H, W, self.cout, self.cin, self.k, [_plain_src(dy)], wt)
+        ws = None   # split-K scratch (L.attach_workspace), attached once every other field is set
         if dgrad["mode"] == "y":
             # op-dtype gradient, stored; with "bnb" (the Act it is the gradient of) the epilogue also
             # reduces that activation's BatchNorm-backward sums, returned in dgrad["bnb_part"]
@@ -259,6 +261,7 @@ class ConvBN:
             if a is not None:
                 d.bnb_y, d.bnb_scale, d.bnb_shift = vp(a.data), vp(a.ab[0]), vp(a.ab[1])
                 d.bnb_relu, d.bnb_mean, d.bnb_invstd = int(a.relu), vp(a.mean), vp(a.invstd)
+                ws = L.attach_workspace(d, dev)
                 rows = L.load().unet_conv_stats_rows(d)
                 part = f32(2, rows, self.cin, device=dev)
                 d.bnb_stats = part.data_ptr()
@@ -286,6 +289,8 @@ class ConvBN:
             o2 = dgrad.get("out2")
             d.out2 = o2.data_ptr() if o2 is not None else None
             d.accum2 = int(dgrad.get("accum2", 0))
+        if ws is None:
+            ws = L.attach_workspace(d, dev)
         probe.launch(lambda: conv_kernel_name(d), 2.0 * N * H * W * self.cin * self.cout * self.k ** 2,
                      lambda: L.call("unet_conv", d, stream()), d.out_mode)
 
