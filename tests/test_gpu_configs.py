@@ -51,6 +51,7 @@ def _assert_16bit_paths(log, prec):
                                                                                       and ",3," in n)]
     assert not bad, sorted(names)
     assert any(n.startswith(f"conv5_kernel<{prec},") and m == 0 for n, m in log), sorted(names)
+    assert any(n == f"conv5w_kernel<{prec}>" and m == 0 for n, m in log), sorted(names)   # round 6: >= 128 channels
     assert any(n.startswith((f"conv5_kernel<{prec},", f"conv3_kernel<{prec},3,")) and m == 1 for n, m in log), \
         sorted(names)
     # the small-map y outputs (down4 at 32^2, up1.conv.3 at 64^2): conv5's small-map forms since round 5 (split-K

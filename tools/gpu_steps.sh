@@ -35,7 +35,7 @@ for step in ${STEPS:-tests smoke bench}; do
   trace)   # kernel-trace stats of the bench command
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-fp32-line --no-graph-line > $O/trace.log 2>&1 || fail trace $O/trace.log
     # 78 traced steps: 5 warm-up + 30 timed + 10 probe + 2 hbm-probe + 31 fwd+bwd-only (without_optimizer)
-    python tools/profsum.py $O/trace 78 45 "conv5_kernelIDF16b|conv3_kernelIDF16bLi3E|unet::conv5_kernel<" "conv5_splitk_finish_kernel" > $O/trace_summary.txt 2>&1; tail -3 $O/trace_summary.txt ;;
+    python tools/profsum.py $O/trace 78 45 "conv5_kernelIDF16b|conv5w_kernelIDF16b|conv3_kernelIDF16bLi3E|unet::conv5_kernel<" "conv5_splitk_finish_kernel" > $O/trace_summary.txt 2>&1; tail -3 $O/trace_summary.txt ;;
   layerprof)
     timeout -k 10 300 python -u tools/layerprof.py > $O/layerprof.txt 2>&1 || fail layerprof $O/layerprof.txt
     tail -5 $O/layerprof.txt ;;

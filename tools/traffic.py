@@ -39,8 +39,8 @@ HBM_FAMILIES = {
     "pw_conv_kernel": r"pw_conv_kernel(.*Li0EEEv|<.*, 0>)",              # OMK 0: y + BN sums
     "pw_conv_kernel(dgrad)": r"pw_conv_kernel(.*Li[12]EEEv|<.*, [12]>)",  # OMK 1 / 2: fp32 / gated fp32
 }
-CONV_FAMILY = {"bf16": r"(conv3_kernel<bf16,3,|conv5_kernel<bf16,|conv3_kernelIDF16bLi3E|conv5_kernelIDF16b)",
-               "fp16": r"(conv3_kernel<fp16,3,|conv5_kernel<fp16,|conv3_kernelIDF16_Li3E|conv5_kernelIDF16_)"}
+CONV_FAMILY = {"bf16": r"(conv3_kernel<bf16,3,|conv5_kernel<bf16,|conv3_kernelIDF16bLi3E|conv5w?_kernelIDF16b)",
+               "fp16": r"(conv3_kernel<fp16,3,|conv5_kernel<fp16,|conv3_kernelIDF16_Li3E|conv5w?_kernelIDF16_)"}
 
 
 def rows_of(d):
@@ -81,11 +81,11 @@ def main():
         fetch, write = per_kernel(rows_of(d1), "FETCH_SIZE"), per_kernel(rows_of(d2), "WRITE_SIZE")
         fams = dict(HBM_FAMILIES)
         for prec, rx in CONV_FAMILY.items():
-            key = f"conv3_kernel<{prec},3,|conv5_kernel<{prec},"
+            key = f"conv3_kernel<{prec},3,|conv5_kernel<{prec},|conv5w_kernel<{prec}>"   # bench.py's family key
             fams[key] = rx
         # every conv5 / conv3 instantiation separately (the conv family's traffic split)
         for k in set(fetch[0]) | set(write[0]):
-            m = re.search(r"(conv5_kernel|conv3_kernel)\S*", k)
+            m = re.search(r"(conv5w_kernel|conv5_kernel|conv3_kernel)\S*", k)
             if m:
                 fams["inst:" + m.group(0)] = re.escape(m.group(0))
         for fam, rx in sorted(fams.items()):

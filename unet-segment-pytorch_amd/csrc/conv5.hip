@@ -35,6 +35,12 @@
 
 namespace unet {
 
+// conv5w.hip: the 128-output-channel form (round 6), preferred wherever it serves
+bool conv5w_ok(const unet_conv_desc* d);
+int conv5w_stats_rows(const unet_conv_desc* d);
+int conv5w_variant(const unet_conv_desc* d, char* buf, int len);
+int conv5w_run(const unet_conv_desc* d, int prio, hipStream_t st);
+
 constexpr int C5_W = 32, C5_HW = 34;     // tile width, halo width (pixels)
 constexpr int C5_WM = 4;                 // wave row groups of a workgroup tile
 constexpr int C5_WH = 2;                 // 32-channel halves of the block's 64 output channels
@@ -84,7 +90,7 @@ struct C5Layout {
 // split == Cout, no accumulation: the host's descriptor); conv5_splitk_finish_kernel sums the slabs in order
 template <typename T, int MI, int OM, int SK, int GATE, int ABL = 0, int PIPE = 1, int NWV = 8, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc d, int tiles_w, int tiles_h,
-                                                           int mtiles, int nch, int nch_all) {
+                                                           int mtiles, int nch, int nch_all, int prio) {
   using F = typename Mma32<T>::frag;
   constexpr bool ACT = SK != SK_PLAIN && SK != SK5_PLAIN1;
   constexpr bool ONE = SK == SK_ACT || SK == SK5_PLAIN1;   // one source, no ragged 16-channel chunk
@@ -490,6 +496,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
     }
   };
   if constexpr (PIPE) load_col(K, 0, xA, wA);
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md, two waves per SIMD, item 4): waves 4-7
+  // share their SIMDs with waves 0-3 and lose every issue arbitration by age
+  if (prio && wave >= NWV / 2) __builtin_amdgcn_s_setprio(1);
   // BNB: the activation y1 of this wave's tile pixels (buffer loads, out-of-range offsets for masked lanes:
   // a fixed count), loaded during the tile's last chunk so that the epilogue's wait for them does not drain
   // the next chunks' DMAs (their issue follows the epilogue).  16-byte loads in the layout of the epilogue's
@@ -926,6 +935,12 @@ static int conv5_mode() {
   return e ? (atoi(e) ? 1 : 0) : 2;
 }
 
+// UNET_C5_PRIO=1: s_setprio 1 for waves 4-7 (A/B; read per call)
+static int conv5_prio() {
+  const char* e = getenv("UNET_C5_PRIO");
+  return e ? atoi(e) : 0;
+}
+
 static long long conv5_mtiles(const unet_conv_desc* d, int mi) {
   return (long long)d->N * cdiv(d->W, C5_W) * cdiv(d->H, C5_WM * mi);
 }
@@ -998,7 +1013,7 @@ bool conv5_eligible(const unet_conv_desc* d) {
 static int conv5_splitk_shape(const unet_conv_desc* d) {
   const char* e = getenv("UNET_CONV5_SPLIT");   // read per call (tests flip it)
   const int on = e ? atoi(e) : 1;
-  if (!on || conv5_mode() == 0 || d->act_out || !conv5_shape_ok(d)) return 1;
+  if (!on || conv5_mode() == 0 || d->act_out || !conv5_shape_ok(d) || conv5w_ok(d)) return 1;
   if (d->Cout > 1024 || (d->Cout & (d->Cout - 1))) return 1;     // the finisher's channel-vector layout
   // a slab is addressed by one buffer resource (32-bit range): the kernel's counted fp32 stores need it
   if ((double)d->N * d->H * d->W * d->Cout * 4 >= (double)OOB) return 1;
@@ -1014,7 +1029,9 @@ static int conv5_splitk_shape(const unet_conv_desc* d) {
 // descriptor without one — e.g. zero-initialised by a C caller — runs the unsplit form, as before round 5)
 int conv5_splitk(const unet_conv_desc* d) { return d->workspace ? conv5_splitk_shape(d) : 1; }
 
-bool conv5_serves(const unet_conv_desc* d) { return conv5_eligible(d) || conv5_splitk(d) > 1; }
+bool conv5_serves(const unet_conv_desc* d) {
+  return (conv5_mode() != 0 && conv5w_ok(d)) || conv5_eligible(d) || conv5_splitk(d) > 1;
+}
 
 size_t conv5_workspace(const unet_conv_desc* d) {
   const int S = conv5_eligible(d) ? 1 : conv5_splitk_shape(d);
@@ -1030,17 +1047,21 @@ static int fin_rows(const unet_conv_desc* d) {
 }
 
 int conv5_stats_rows(const unet_conv_desc* d) {
+  if (conv5_mode() != 0 && conv5w_ok(d)) return conv5w_stats_rows(d);
   if (!conv5_eligible(d) && conv5_splitk(d) > 1) return fin_rows(d);
   return conv5_gx(d, conv5_mi(d)) * C5_WM;
 }
 
 // can the forward write src[0]'s transformed input to act_out (the y-mode BN-activation kernel serves d)?
 bool conv5_act_out_ok(const unet_conv_desc* d) {
+  if (conv5_mode() != 0 && conv5w_ok(d))
+    return d->out_mode == UNET_OUT_Y && !d->bnb_stats && d->src[0].kind == UNET_SRC_ACT;
   return conv5_eligible(d) && d->out_mode == UNET_OUT_Y && !d->bnb_stats && d->src[0].kind == UNET_SRC_ACT &&
          d->src[0].C % 16 == 0;
 }
 
 int conv5_variant(const unet_conv_desc* d, char* buf, int len) {
+  if (conv5_mode() != 0 && conv5w_ok(d)) return conv5w_variant(d, buf, len);
   const int S = conv5_eligible(d) ? 1 : conv5_splitk(d);
   const int mi = conv5_mi(d);
   if (S > 1) snprintf(buf, len, "conv5_kernel<%s,%d>+splitk%d", d->dtype == UNET_F16 ? "fp16" : "bf16", mi, S);
@@ -1066,7 +1087,7 @@ static int launch5_mi(const unet_conv_desc* d, hipStream_t st) {
   const int gx = conv5_gx(d, MI);
   const int nch = cdiv(d->Cin, 16);
   hipLaunchKernelGGL((conv5_kernel<T, MI, OM, SK, GATE, ABL, PIPE, 8>), dim3(gx, gy), dim3(512), 0, st, *d, tw, th,
-                     mt, nch, nch);
+                     mt, nch, nch, conv5_prio());
   return check_launch("conv5");
 }
 template <typename T, int OM, int SK, int GATE, int ABL = 0, int PIPE_ = -1>
@@ -1116,7 +1137,7 @@ static int launch5_split_mi(const unet_conv_desc* d, int S, hipStream_t st) {
   k.bnb_stats = nullptr;
   k.act_out = nullptr;
   hipLaunchKernelGGL((conv5_kernel<T, MI, OM5_F32, SK, GATE, 0, 1, 8, true>), dim3(mt, gy, S), dim3(512), 0, st, k,
-                     tw, th, mt, nch / S, nch);
+                     tw, th, mt, nch / S, nch, conv5_prio());
   if (int e = check_launch("conv5 split")) return e;
   return launch5_finish<T>(d, S, st);
 }
@@ -1160,6 +1181,7 @@ static int dispatch5(const unet_conv_desc* d, hipStream_t st) {
 }
 
 int conv5_run(const unet_conv_desc* d, hipStream_t st) {
+  if (conv5_mode() != 0 && conv5w_ok(d)) return conv5w_run(d, conv5_prio(), st);
   return d->dtype == UNET_F16 ? dispatch5<f16>(d, st) : dispatch5<bf16>(d, st);
 }
 
@@ -1202,7 +1224,7 @@ static int abl5_split_mi(const unet_conv_desc* d, int abl, hipStream_t st) {
   k.bnb_stats = nullptr;
   k.act_out = nullptr;
   const dim3 grid(mt, gy, S);
-#define C5SA(A) hipLaunchKernelGGL((conv5_kernel<bf16, MI, OM5_F32, SK, 0, A, 1, 8, true>), grid, dim3(512), 0, st, k, tw, th, mt, nch / S, nch)
+#define C5SA(A) hipLaunchKernelGGL((conv5_kernel<bf16, MI, OM5_F32, SK, 0, A, 1, 8, true>), grid, dim3(512), 0, st, k, tw, th, mt, nch / S, nch, 0)
   switch (abl) {
     case 0: C5SA(0); break;
     case 1: C5SA(1); break;
