@@ -122,3 +122,61 @@ def test_conv5w_dgrad_f32_matches_conv5(prec, split, shape, monkeypatch):
     assert v1 == f"conv5w_kernel<{TN[prec]}>" and v0.startswith("conv5_kernel"), (v1, v0)
     assert torch.isfinite(a1).all()
     assert torch.equal(a1, a0) and (split == "whole" or torch.equal(b1, b0))
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 256, 128, 128), (4, 256, 256, 64, 128), (4, 128, 128, 256, 256),
+                                   (3, 200, 328, 64, 128)], ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("relu", [1, 0])
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_conv5w_dgrad_bnb_matches_conv5(prec, relu, shape, monkeypatch):
+    """The middle-activation dgrad with the BN-backward sums in its epilogue (dy[cout] -> g[cmid], cmid >= 128):
+    g bit-identical to conv5's, the per-row sums' totals equal to fp32 summation order."""
+    L, R = _lib(), _rt()
+    N, H, W, cout, cmid = shape     # the dgrad conv: Cin = cout (dy channels), Cout = cmid
+    dt = DT[prec]
+    torch.manual_seed(53)
+    dy = _rand(N, H, W, cout, dt=dt)
+    y1 = _rand(N, H, W, cmid, dt=dt)
+    ab = torch.stack([torch.rand(cmid, device="cuda") + 0.5, torch.randn(cmid, device="cuda") * 0.2])
+    mean = torch.randn(cmid, device="cuda") * 0.1
+    invstd = torch.rand(cmid, device="cuda") + 0.5
+    w = (torch.randn(cout, cmid, 3, 3, device="cuda") * (2.0 / (9 * cmid)) ** 0.5).to(dt).float()
+    P = R._PRECISIONS[prec]
+    wp = R.pack_weight(w, P, transpose=True)
+    src = L.Src()
+    src.kind, src.C, src.H, src.W, src.data = L.SRC_PLAIN, cout, H, W, dy.data_ptr()
+    monkeypatch.setenv("UNET_CONV5", "1")
+    res = {}
+    for wide in ("1", "0"):
+        monkeypatch.setenv("UNET_CONV5W", wide)
+        g = torch.full((N, H, W, cmid), float("nan"), dtype=dt, device="cuda")
+        d = L.ConvDesc()
+        d.dtype = P.code
+        d.N, d.H, d.W, d.Cin, d.Cout, d.ksize, d.nsrc = N, H, W, cout, cmid, 3, 1
+        d.src[0] = src
+        d.weight = wp.data_ptr()
+        d.out_mode = L.OUT_Y
+        d.out = g.data_ptr()
+        d.bnb_y, d.bnb_scale, d.bnb_shift, d.bnb_relu = y1.data_ptr(), ab[0].data_ptr(), ab[1].data_ptr(), relu
+        d.bnb_mean, d.bnb_invstd = mean.data_ptr(), invstd.data_ptr()
+        ws = L.attach_workspace(d, "cuda")
+        rows = L.load().unet_conv_stats_rows(d)
+        part = torch.full((2, rows, cmid), float("nan"), device="cuda")
+        d.bnb_stats = part.data_ptr()
+        L.call("unet_conv", d, R.stream())
+        torch.cuda.synchronize()
+        res[wide] = (_variant(d), g, part.double().sum(1))
+        del ws
+    (v1, g1, s1), (v0, g0, s0) = res["1"], res["0"]
+    assert v1 == f"conv5w_kernel<{TN[prec]}>" and v0.startswith("conv5_kernel"), (v1, v0)
+    assert torch.isfinite(g1.float()).all()
+    assert torch.equal(g1, g0)
+    # reference sums of the stored gradient (fp64): sum g' and sum g' * (y1 - mean) * invstd, g' = g masked by ReLU
+    gg = g0.double()
+    if relu:
+        gg = torch.where(y1.double() * ab[0].double() + ab[1].double() > 0, gg, torch.zeros_like(gg))
+    ref0 = gg.reshape(-1, cmid).sum(0)
+    ref1 = (gg * (y1.double() - mean.double()) * invstd.double()).reshape(-1, cmid).sum(0)
+    for got, ref in ((s1[0], ref0), (s1[1], ref1), (s0[0], ref0), (s0[1], ref1)):
+        assert torch.isfinite(got).all()
+        assert ((got - ref).abs() <= 1e-4 * gg.abs().reshape(-1, cmid).sum(0) + 1e-3).all(), float((got - ref).abs().max())

@@ -52,10 +52,10 @@ constexpr int W5_WPW = (W5_NWF + 7) / 8;    // per wave (5; 4 of the 40 go to th
 constexpr int W5_WIMG = W5_NWF * 1024;
 constexpr int W5_CMAX = 1024;               // largest BN-activation source
 constexpr int W5_TABS = W5_CMAX + 8;        // scale / shift table stride (each half zero-padded)
-constexpr int W5_OM_Y = 0, W5_OM_F32 = 1;
+constexpr int W5_OM_Y = 0, W5_OM_F32 = 1, W5_OM_BNB = 2;
 constexpr int W5_SK_PLAIN1 = 4;             // = conv5.hip's SK5_PLAIN1: one stored source, C % 16 == 0
 
-template <bool ACT, bool GATED>
+template <bool ACT, bool GATED, bool BNB>
 struct W5Lay {
   static constexpr int NCOMP = ACT ? 2 : 3;
   static constexpr int OFF_COMP = 0;
@@ -63,13 +63,15 @@ struct W5Lay {
   static constexpr int OFF_W = OFF_RAW + (ACT ? W5_IMG : 0);
   static constexpr int OFF_GATE = OFF_W + 2 * W5_WIMG;
   static constexpr int OFF_TAB = OFF_GATE + (GATED ? W5_NI * 256 : 0);
-  static constexpr int OFF_JUNK = OFF_TAB + (ACT ? 2 * W5_TABS * 4 : 0);
+  static constexpr int OFF_BTAB = OFF_TAB + (ACT ? 2 * W5_TABS * 4 : 0);   // BNB: the block's BN affine
+  static constexpr int OFF_JUNK = OFF_BTAB + (BNB ? 2 * W5_BN * 4 : 0);
   static constexpr int BYTES = OFF_JUNK + 1024;
   static_assert(BYTES <= 160 * 1024, "conv5w LDS");
 };
 
 // SK: W5_SK_PLAIN1 (stored, one source), SK_ACT (one BN activation, GATE: attention-gated) or SK_ACT_PLAIN
-// (src0 BN activation (+gate), src1 stored: the up-block concat); OM: W5_OM_Y or W5_OM_F32 (PLAIN1 only)
+// (src0 BN activation (+gate), src1 stored: the up-block concat); OM: W5_OM_Y, W5_OM_F32 or W5_OM_BNB (y + the
+// BN-backward sums of the activation whose gradient this dgrad writes; the last two with PLAIN1 only)
 template <typename T, int OM, int SK, int GATE>
 __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, int tiles_w, int tiles_h, int mtiles,
                                                         int nch, int prio) {
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
   constexpr bool ACT = SK != W5_SK_PLAIN1;
   constexpr bool ONE = SK != SK_ACT_PLAIN;
   constexpr bool GATED = ACT && GATE;
-  using Lay = W5Lay<ACT, GATED>;
+  using Lay = W5Lay<ACT, GATED, OM == W5_OM_BNB>;
   constexpr int MI = W5_MI, TH = W5_TH, NI = W5_NI, DPW = W5_DPW, WPW = W5_WPW, NS = W5_NS;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[Lay::BYTES];
 
@@ -307,6 +309,16 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
     for (int c = tid; c < C0; c += 512) { tab[c] = s0.scale[c]; tab[W5_TABS + c] = s0.shift[c]; }
     if (tid < 8) { tab[C0 + tid] = 0.f; tab[W5_TABS + C0 + tid] = 0.f; }
   }
+  if constexpr (OM == W5_OM_BNB) {
+    // the BN affine of the activation whose gradient this dgrad writes (its ReLU mask), the block's channels
+    float* bt = reinterpret_cast<float*>(lds + Lay::OFF_BTAB);
+    if (tid < W5_BN) {
+      const int co = (int)blockIdx.y * W5_BN + tid;
+      const bool ok = co < d.Cout && d.bnb_relu;
+      bt[tid] = ok ? d.bnb_scale[co] : 0.f;
+      bt[W5_BN + tid] = ok ? d.bnb_shift[co] : 0.f;
+    }
+  }
   Cur I, K;   // I: next chunk to DMA (halo); K: chunk being computed
   cur_init(I);
   cur_init(K);
@@ -385,12 +397,17 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
   };
 
   // the vmcnt waits: what may stay in flight is counted from the issue order (file header)
-  constexpr int NST = OM == W5_OM_Y ? 2 * MI : 4 * MI;   // epilogue stores per tile
+  constexpr int NST = OM == W5_OM_F32 ? 4 * MI : 2 * MI;   // epilogue stores per tile
+  // BNB: the tile's last DMA batch is issued after its epilogue (behind the y1 loads' wait), so the epilogue's
+  // stores are older than the next wait's batch: none of them may stay in flight there
+  constexpr int NSTW = OM == W5_OM_BNB ? 0 : NST;
   constexpr int NSA = (ACT && OM == W5_OM_Y) ? DPW : 0;  // act_out stores per transform
   bool st = false;   // the previous chunk ended a tile: its NST epilogue stores are the youngest
   int g = 0;
   const bool f32c = OM == W5_OM_F32;
-  const rsrc_t ry = mk_rsrc(d.out, (unsigned)(OM == W5_OM_Y ? npix * d.Cout * 2 : 0));
+  const rsrc_t ry = mk_rsrc(d.out, (unsigned)(OM != W5_OM_F32 ? npix * d.Cout * 2 : 0));
+  const rsrc_t ry1 = mk_rsrc(OM == W5_OM_BNB ? d.bnb_y : d.out, (unsigned)(OM == W5_OM_BNB ? npix * d.Cout * 2 : 0));
+  bool pend_w = false, pend_h = false;   // BNB: the deferred DMA issues of a tile's last chunk
   const rsrc_t rf1 = mk_rsrc(d.out, (unsigned)(f32c ? npix * d.split * 4 : 0));
   const rsrc_t rf2 = mk_rsrc(d.out2 ? d.out2 : d.out, (unsigned)(f32c ? npix * (d.Cout - d.split) * 4 : 0));
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
@@ -439,16 +456,22 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
         }
       } else {
         // H(g+1) and W(g+1) landed: H(g+2) (issued with W(g+1)) and the epilogue stores may stay in flight
-        if (st) { if (h2) wait_vm<NST + DPW>(); else wait_vm<NST>(); }
+        if (st && NSTW) { if (h2) wait_vm<NSTW + DPW>(); else wait_vm<NSTW>(); }
         else { if (h2) wait_vm<DPW>(); else wait_vm<0>(); }
         lds_barrier();
-        if (h2) {
-          issue_w(IW);
-          wcur_next(IW);
-        }
-        if (g + 3 < G) {
-          issue_h(I);
-          cur_next(I);
+        const bool h3 = g + 3 < G;
+        if (OM == W5_OM_BNB && c == nch - 1) {
+          pend_w = h2;
+          pend_h = h3;
+        } else {
+          if (h2) {
+            issue_w(IW);
+            wcur_next(IW);
+          }
+          if (h3) {
+            issue_h(I);
+            cur_next(I);
+          }
         }
       }
       st = false;
@@ -510,6 +533,69 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
           sB[r] = b2.x; sB[r + 1] = b2.y;
         }
       }
+    } else if constexpr (OM == W5_OM_BNB) {
+      // per 16-channel half h: y1 of this wave's pixels, 16-byte loads in the layout of the swapped g stores
+      // (lanes 0-31 channels 16h + 0..7 of their pixel, lanes 32-63 16h + 8..15; one half at a time: 32
+      // registers); the compiler's wait for them also covers the older DMAs, all issued a chunk or more ago
+      const float* btab = reinterpret_cast<const float*>(lds + Lay::OFF_BTAB);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int co = cw0 + 16 * h + 8 * hh;
+        const bool cok = co < d.Cout;
+        const int cb = co - (int)blockIdx.y * W5_BN;
+        uint4 yv[MI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const bool ok = colok && i < rows && cok;
+          const unsigned vo = ok ? ((pix0 + (unsigned)i * d.W) * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
+          yv[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ry1, (int)vo, 0, 0));
+        }
+        float sc8[8], sf8[8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float4 a4 = *reinterpret_cast<const float4*>(btab + cb + 4 * q);
+          const float4 b4 = *reinterpret_cast<const float4*>(btab + W5_BN + cb + 4 * q);
+          sc8[4 * q] = a4.x; sc8[4 * q + 1] = a4.y; sc8[4 * q + 2] = a4.z; sc8[4 * q + 3] = a4.w;
+          sf8[4 * q] = b4.x; sf8[4 * q + 1] = b4.y; sf8[4 * q + 2] = b4.z; sf8[4 * q + 3] = b4.w;
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const unsigned pix = pix0 + (unsigned)i * d.W;
+          const bool ok = colok && i < rows && cok;
+          const int g0 = 2 * h;
+          const unsigned pxa = pack2_16<T>(acc[i][4 * g0], acc[i][4 * g0 + 1]);
+          const unsigned pxb = pack2_16<T>(acc[i][4 * g0 + 4], acc[i][4 * g0 + 5]);
+          const unsigned pya = pack2_16<T>(acc[i][4 * g0 + 2], acc[i][4 * g0 + 3]);
+          const unsigned pyb = pack2_16<T>(acc[i][4 * g0 + 6], acc[i][4 * g0 + 7]);
+          const auto sx = __builtin_amdgcn_permlane32_swap(pxa, pxb, false, false);
+          const auto sy = __builtin_amdgcn_permlane32_swap(pya, pyb, false, false);
+          const unsigned vo = ok ? (pix * (unsigned)d.Cout + (unsigned)co) * 2u : OOB;
+          const u32x4_t v4 = {sx[0], sy[0], sx[1], sy[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(v4, ry, (int)vo, 0, 0);
+          if (ok) {
+            float gv[8], yy[8];
+            unpack4_16<T>(make_uint2(v4[0], v4[1]), gv);
+            unpack4_16<T>(make_uint2(v4[2], v4[3]), gv + 4);
+            unpack4_16<T>(make_uint2(yv[i].x, yv[i].y), yy);
+            unpack4_16<T>(make_uint2(yv[i].z, yv[i].w), yy + 4);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              const float gg = (d.bnb_relu && !(yy[r] * sc8[r] + sf8[r] > 0.f)) ? 0.f : gv[r];
+              sA[8 * h + r] += gg;
+              sB[8 * h + r] = __builtin_fmaf(gg, yy[r], sB[8 * h + r]);
+            }
+          }
+        }
+      }
+      if (pend_w) {
+        issue_w(IW);
+        wcur_next(IW);
+      }
+      if (pend_h) {
+        issue_h(I);
+        cur_next(I);
+      }
+      pend_w = pend_h = false;
     } else {   // fp32 gradient, counted buffer stores (no accumulation: host-checked), split at d.split
       const int c2 = d.Cout - d.split;
 #pragma unroll
@@ -546,6 +632,29 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
         }
       }
     }
+  } else if constexpr (OM == W5_OM_BNB) {
+    // one [rows][Cout] partial row per wave row group; sum slot 8h + r is channel cw0 + 16h + 8hh + r
+    const int hh = lane >> 5;
+    const int srow = blockIdx.x * W5_WM + wm, srows = gridDim.x * W5_WM;
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int co = cw0 + 16 * (gq >> 1) + 8 * hh + 4 * (gq & 1);
+      float a[4], b[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = half32_sum(sA[4 * gq + r]);
+        b[r] = half32_sum(sB[4 * gq + r]);
+      }
+      if ((lane & 31) == 0 && co < d.Cout) {
+        const float4 m4 = *reinterpret_cast<const float4*>(d.bnb_mean + co);
+        const float4 i4 = *reinterpret_cast<const float4*>(d.bnb_invstd + co);
+        const float mu[4] = {m4.x, m4.y, m4.z, m4.w}, is[4] = {i4.x, i4.y, i4.z, i4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[r] = is[r] * (b[r] - mu[r] * a[r]);
+        *reinterpret_cast<float4*>(d.bnb_stats + (size_t)srow * d.Cout + co) = make_float4(a[0], a[1], a[2], a[3]);
+        *reinterpret_cast<float4*>(d.bnb_stats + ((size_t)srows + srow) * d.Cout + co) = make_float4(b[0], b[1], b[2], b[3]);
+      }
+    }
   }
 }
 
@@ -559,7 +668,9 @@ bool conv5w_ok(const unet_conv_desc* d) {
   const char* e = getenv("UNET_CONV5W");
   if (e && !atoi(e)) return false;
   if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 3) return false;
-  if (d->Cout % W5_BN || d->Cin < 32 || d->Cin % 16 || d->bnb_stats) return false;
+  if (d->Cout % W5_BN || d->Cin < 32 || d->Cin % 16) return false;
+  if (d->bnb_stats && (d->out_mode != UNET_OUT_Y || d->nsrc != 1 || d->src[0].kind != UNET_SRC_PLAIN || !d->bnb_y))
+    return false;
   const unet_src& s0 = d->src[0];
   if (d->nsrc < 1 || d->nsrc > 2) return false;
   if (s0.kind != UNET_SRC_PLAIN && s0.kind != UNET_SRC_ACT) return false;
@@ -616,6 +727,7 @@ template <typename T>
 static int dispatch5w(const unet_conv_desc* d, int prio, hipStream_t st) {
   const unet_src& s0 = d->src[0];
   if (d->out_mode == UNET_OUT_F32) return launch5w<T, W5_OM_F32, W5_SK_PLAIN1, 0>(d, prio, st);
+  if (d->bnb_stats) return launch5w<T, W5_OM_BNB, W5_SK_PLAIN1, 0>(d, prio, st);
   if (s0.kind == UNET_SRC_PLAIN) return launch5w<T, W5_OM_Y, W5_SK_PLAIN1, 0>(d, prio, st);
   const bool g = s0.gate_p != nullptr;
   if (d->nsrc == 1) return g ? launch5w<T, W5_OM_Y, SK_ACT, 1>(d, prio, st) : launch5w<T, W5_OM_Y, SK_ACT, 0>(d, prio, st);
