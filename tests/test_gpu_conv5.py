@@ -21,14 +21,15 @@ Y_SHAPES = [(4, 512, 512, 64, 64), (4, 256, 256, 64, 128), (4, 256, 256, 128, 12
 PATH = {"conv5": {"UNET_CONV5": "1"}}
 
 
-def _wide(N, H, W, cout, mode="y", accum=False):
-    """conv5w (csrc/conv5w.hip, round 6) serves the >= 128-channel outputs whose 16 x 32 x 128 tiles fill the chip
-    (fp32 gradients only without accumulation)"""
-    return cout % 128 == 0 and N * -(-W // 32) * -(-H // 16) * (cout // 128) >= 256 and not (mode == "f32" and accum)
+def _wide(N, H, W, cin, cout, mode="y", src="plain"):
+    """conv5w (csrc/conv5w.hip, round 6) serves, by default, the BN-activation forwards with >= 256 input channels
+    and >= 128 output channels whose 16 x 32 x 128 tiles fill the chip (conv5w_ok)"""
+    return (mode == "y" and src != "plain" and cin >= 256 and cout % 128 == 0
+            and N * -(-W // 32) * -(-H // 16) * (cout // 128) >= 256)
 
 
-def _want(prec, cout, path, shape=None, mode="y", accum=False):
-    if shape is not None and _wide(shape[0], shape[1], shape[2], cout, mode, accum):
+def _want(prec, cout, path, shape=None, mode="y", src="plain"):
+    if shape is not None and _wide(shape[0], shape[1], shape[2], shape[3], cout, mode, src):
         return f"conv5w_kernel<{TN[prec]}>"
     return f"conv5_kernel<{TN[prec]},4>"
 
@@ -84,7 +85,7 @@ def test_conv5_y_stats(prec, src, shape, path):
     st = torch.full((2, cout, rows), float("nan"), device="cuda")
     out = torch.empty(N, H, W, cout, dtype=dt, device="cuda")
     d = _conv(prec, srcs, N, H, W, cin, w, 3, L.OUT_Y, out=out.data_ptr(), stats=st.data_ptr())
-    assert _variant(d) == _want(prec, cout, path, shape), _variant(d)
+    assert _variant(d) == _want(prec, cout, path, shape, "y", src), _variant(d)
     ref = F.conv2d(x.permute(0, 3, 1, 2), w, padding=1).permute(0, 2, 3, 1)
     _close_bf16(out.float(), ref, "y")
     r = ref.double().reshape(-1, cout)
@@ -117,7 +118,7 @@ def test_conv5_dgrad_f32_split_accum(prec, shape, path):
     o2 = torch.full((N, H, W, cin - split), float("nan"), device="cuda")
     d = _conv(prec, [src], N, H, W, cout, w, 3, L.OUT_F32, transpose=True, out=o1.data_ptr(), out2=o2.data_ptr(),
               split=split, accum=1, accum2=0)
-    assert _variant(d) == _want(prec, cin, path, shape, "f32", True), _variant(d)
+    assert _variant(d) == _want(prec, cin, path, shape, "f32"), _variant(d)
     _close_bf16(torch.cat([o1 - 0.5, o2], -1), ref, "dgrad f32")
     # unsplit, stored
     o = torch.full((N, H, W, cin), float("nan"), device="cuda")

@@ -663,10 +663,24 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
 // ------------------------------------------------------------------------------------------------
 static long long w5_mtiles(const unet_conv_desc* d) { return (long long)d->N * cdiv(d->W, W5_W) * cdiv(d->H, W5_TH); }
 
-// UNET_CONV5W=0: never (A/B against conv5 / conv3); read per call so tests can flip it
-bool conv5w_ok(const unet_conv_desc* d) {
+// UNET_CONV5W: unset = the measured default (below), 0 = never, 1 = every descriptor it can serve (tests, A/B);
+// read per call so tests can flip it
+static int conv5w_mode() {
   const char* e = getenv("UNET_CONV5W");
-  if (e && !atoi(e)) return false;
+  return e ? (atoi(e) ? 1 : 0) : 2;
+}
+
+bool conv5w_ok(const unet_conv_desc* d) {
+  const int mode = conv5w_mode();
+  if (mode == 0) return false;
+  // default: the BN-activation forwards with >= 256 input channels (the gated [skip, up] concats, down2.3):
+  // -5 to -23 us per layer against conv5, which stages and transforms every chunk twice there.  Measured
+  // slower (round 6, profiles/r06_layerprof_conv5w*.txt): the BNB dgrads (+10 to +28 us: its y1 loads cannot
+  // be issued during the last chunk, so the tile's next DMAs wait behind them), the stored-source forwards and
+  // any layer with few chunk steps per workgroup (+2 to +5 us: a chunk of this form is twice conv5's, so the
+  // pipeline's fill and drain cost twice as much), and the fp32 dgrads (even with conv3)
+  if (mode == 2 && (d->out_mode != UNET_OUT_Y || d->bnb_stats || d->src[0].kind != UNET_SRC_ACT || d->Cin < 256))
+    return false;
   if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 3) return false;
   if (d->Cout % W5_BN || d->Cin < 32 || d->Cin % 16) return false;
   if (d->bnb_stats && (d->out_mode != UNET_OUT_Y || d->nsrc != 1 || d->src[0].kind != UNET_SRC_PLAIN || !d->bnb_y))
