@@ -141,33 +141,32 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
   // scalar work — the scalar unit is shared by the CU's 8 waves, and a version with per-slot exec branches,
   // divisions for the tile geometry and a switch over the wait count issued ~360 SALU per 36 MFMAs per
   // wave (SQ_INSTS_SALU), which paced the loop
-  int hbit[DPW];        // logical channel half of the slot (swizzled image)
+  // Round 6: the compute image's swizzle is by the pixel's halo COLUMN x (x >> 3 & 1 flips the two 16-byte
+  // channel halves), not by its image index, so a halo row is a fixed 1088-byte stride and the B fragments are
+  // addressed by one base register per tap column plus an immediate per row (round 5: 18 offset registers and a
+  // v_add per ds_read).  A plain source DMAs each slot's swizzled half directly; a BN-activation source lands
+  // unswizzled (half = lane & 1: one scale / shift read per chunk) and its transform stores slot s ^ swz
+  int hbit[DPW];        // channel half this lane's slot loads
   int soy[DPW], sox[DPW];   // the slot's pixel offset from the tile origin (halo: -1 .. TH, -1 .. 32)
+  unsigned cso[ACT ? DPW : 1];   // ACT: the transformed slot's byte offset in the compute image
 #pragma unroll
   for (int k = 0; k < DPW; ++k) {
     const int i = wave + k * NWV, s = i * 64 + lane;
-    const int hp = s >> 1;
-    // = (lane & 1) ^ ((lane >> 4) & 1) for every k and wave (s and hp move by multiples of 512 / 256 with k,
-    // 64 / 32 with the wave): written in that form so the compiler sees one value (one scale / shift read per chunk)
-    hbit[k] = (lane & 1) ^ ((lane >> 4) & 1);
-    (void)hp;
+    const int hp = s >> 1, x = hp % C5_HW, sw = (x >> 3) & 1;
+    hbit[k] = ACT ? (lane & 1) : ((s & 1) ^ sw);
+    if constexpr (ACT) cso[k] = (unsigned)(s ^ sw) * 16u;
     soy[k] = s < NS ? hp / C5_HW - 1 : -(1 << 20);    // past the image: never a valid row
-    sox[k] = hp % C5_HW - 1;
+    sox[k] = x - 1;
   }
   constexpr int ND = DPW + WPW;   // DMA instructions per wave per chunk (without gate loads)
 
-  // B-fragment byte offsets in a compute image: row r = wm*MI + rr (rr < MI+2), tap column dx
-  unsigned xoff[3][MI + 2];
+  // B-fragment byte offsets in a compute image: tap column dx, row wm*MI (row rr adds rr * 1088, an immediate)
+  unsigned boff[3];
 #pragma unroll
-  for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-    for (int rr = 0; rr < MI + 2; ++rr) {
-      const int hp = (wm * MI + rr) * C5_HW + (lane & 31) + dx;
-      xoff[dx][rr] = (unsigned)(2 * hp + ((lane >> 5) ^ ((hp >> 3) & 1))) * 16u;
-      // opaque to the optimiser: otherwise it splits each offset into two registers and spends two VALU
-      // (v_or + v_add) per B-fragment read instead of one v_add of the ring slot's base
-      asm volatile("" : "+v"(xoff[dx][rr]));
-    }
+  for (int dx = 0; dx < 3; ++dx) {
+    const int x = (lane & 31) + dx;
+    boff[dx] = (unsigned)(wm * MI * 2 * C5_HW * 16 + 32 * x + 16 * ((lane >> 5) ^ ((x >> 3) & 1)));
+  }
 
   // ring slots: compute images (PLAIN: 3 = chunk % 3; ACT: 2 = chunk & 1), raw images (ACT: chunk & 1),
   // weights (chunk % 3), gate pre-activations (tile & 1)
@@ -310,8 +309,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
     const unsigned char* rb = raw_buf(q.s2);
     unsigned char* cb = comp_buf(q.s2);
     const float* tab = reinterpret_cast<const float*>(lds + Lay::OFF_TAB);
-    // this lane's 8 channels' scale / shift, read once per chunk (hbit is the same for all its slots; the
-    // compiler would re-read them per slot: the slot's LDS store may alias the table as far as it knows)
+    // this lane's 8 channels' scale / shift, read once per chunk (an activation source's slots all load the
+    // lane's half lane & 1; the compiler would re-read them per slot: the stores may alias the table)
     f2_t sc[4], sf[4];
     if (act) {
       const int ch = cn0 + 8 * hbit[0];             // < C0 + 8: the table is zero-padded there
@@ -359,7 +358,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, q4), rao, (int)vo, 0, 0);
         }
       }
-      *reinterpret_cast<uint4*>((live ? cb : lds) + so) = q4;
+      if constexpr (ACT) *reinterpret_cast<uint4*>(live ? cb + cso[k] : lds + so) = q4;
     }
     if constexpr (OM == OM5_Y) ns_prev = act;
   };
@@ -418,7 +417,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv5_kernel(const unet_conv_desc
     const unsigned char* xb = comp_buf(ACT ? q.s2 : q.s3);
     const unsigned char* wb = w_buf(q.s3) + wn * NJ * 1024 + lane * 16;
 #pragma unroll
-    for (int rr = 0; rr < MI + 2; ++rr) x[rr] = *reinterpret_cast<const F*>(xb + xoff[dx][rr]);
+    for (int rr = 0; rr < MI + 2; ++rr) x[rr] = *reinterpret_cast<const F*>(xb + boff[dx] + rr * (2 * C5_HW * 16));
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
