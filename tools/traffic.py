@@ -36,8 +36,9 @@ HBM_FAMILIES = {
     "unet_materialize": r"materialize_(fast_)?kernel",
     "unet_materialize_pool": r"materialize_pool_kernel",
     "smallcin_fwd_mfma_kernel": r"smallcin_fwd_mfma_kernel",
-    "pw_conv_kernel": r"pw_conv_kernel(.*Li0EEEv|<.*, 0>)",              # OMK 0: y + BN sums
-    "pw_conv_kernel(dgrad)": r"pw_conv_kernel(.*Li[12]EEEv|<.*, [12]>)",  # OMK 1 / 2: fp32 / gated fp32
+    # template <T, NA, NB, OMK, XD> (round 6: XD, the x prefetch depth, after OMK)
+    "pw_conv_kernel": r"pw_conv_kernel(IDF16.?Li\d+ELi\d+ELi0E|<[^>]*, 0, \d+>)",        # OMK 0: y + BN sums
+    "pw_conv_kernel(dgrad)": r"pw_conv_kernel(IDF16.?Li\d+ELi\d+ELi[12]E|<[^>]*, [12], \d+>)",  # OMK 1/2: fp32
 }
 CONV_FAMILY = {"bf16": r"(conv3_kernel<bf16,3,|conv5_kernel<bf16,|conv3_kernelIDF16bLi3E|conv5w?_kernelIDF16b)",
                "fp16": r"(conv3_kernel<fp16,3,|conv5_kernel<fp16,|conv3_kernelIDF16_Li3E|conv5w?_kernelIDF16_)"}

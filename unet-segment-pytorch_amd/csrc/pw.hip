@@ -52,7 +52,12 @@ __device__ __forceinline__ typename Mma<T>::frag pw_act(uint4 q, bool act, const
 // attention gate's W_x input gradient, with the x*s term of the same gradient added here instead of by
 // gate_bwd1: d(x*s) and s = sigmoid(psi) are loaded ahead of the MFMAs).  Distinct instantiations also keep
 // the forward and the dgrads apart in kernel traces and PMC passes (tools/traffic.py)
-template <typename T, int NA, int NB, int OMK>
+// XD (round 6): the x vectors are loaded XD chunk steps ahead (a ring of XD register sets; XD divides nchunks, so
+// a tile's last steps prefetch the next tile's first XD chunks into the same ring slots).  With one step ahead,
+// a wave had ~2 KB of x in flight per memory round trip: the small maps (one or two 32-pixel tiles per wave,
+// 8-16 chunks each) ran latency-bound at 0.8-1.5 TB/s.  The weights and scale / shift (L2-resident) stay one
+// step ahead.
+template <typename T, int NA, int NB, int OMK, int XD>
 __global__ __launch_bounds__(256, 2) void pw_conv_kernel(const unet_conv_desc d, long long P, int nchunks) {
   constexpr bool GATED = OMK == 2;
   typedef typename Mma<T>::frag F;
@@ -79,19 +84,18 @@ __global__ __launch_bounds__(256, 2) void pw_conv_kernel(const unet_conv_desc d,
   // (round 5: the weights and scale / shift were loaded by the step that used them, and a tile's first x
   // chunk at its start: ~3 memory round trips per 64-pixel tile, 5.8 us per tile per wave at 512^2)
   const bool gate = act && s.gate_p != nullptr;
-  unsigned xoff[NB];
-  float gp[NB], gok[NB], gm[NB];
-  auto setup = [&](long long t, uint4 (&xv)[NB]) {
+  unsigned xoff[NB], xoffn[NB];
+  float gp[NB], gok[NB], gm[NB], gpn[NB], gokn[NB];
+  // a tile's pixel offsets / validity / gate pre-activations (no x loads)
+  auto setup = [&](long long t, unsigned (&xo)[NB], float (&go)[NB], float (&gq)[NB]) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const long long p = t * (16 * NB) + 16 * b + i16;
       const bool ok = t < ntiles && p < P;
-      xoff[b] = ok ? (unsigned)p * pixb + (unsigned)g * 16u : PW_OOB;
-      gok[b] = ok ? 1.f : 0.f;
-      gp[b] = (ok && gate) ? s.gate_p[p] : 0.f;
+      xo[b] = ok ? (unsigned)p * pixb + (unsigned)g * 16u : PW_OOB;
+      go[b] = ok ? 1.f : 0.f;
+      gq[b] = (ok && gate) ? s.gate_p[p] : 0.f;
     }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) xv[b] = pw_ld(xr, xoff[b], 0);
   };
   auto stage = [&](int c, uint4 (&wv)[NA], float4 (&scv)[2], float4 (&sfv)[2]) {
 #pragma unroll
@@ -105,9 +109,13 @@ __global__ __launch_bounds__(256, 2) void pw_conv_kernel(const unet_conv_desc d,
       sfv[1] = *reinterpret_cast<const float4*>(s.shift + ch + 4);
     }
   };
-  uint4 xq[NB], wq[NA];
+  uint4 xq[XD][NB], wq[NA];
   float4 scq[2], sfq[2];
-  setup(tile, xq);
+  setup(tile, xoff, gok, gp);
+#pragma unroll
+  for (int u = 0; u < XD; ++u)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) xq[u][b] = pw_ld(xr, xoff[b], (unsigned)u * 64u);   // XD <= nchunks
   stage(0, wq, scq, sfq);
 
   float sm[NA][4], sq[NA][4];   // OMK 0: BN partial sums over all of this wave's tiles (pixels past P add 0)
@@ -162,34 +170,39 @@ __global__ __launch_bounds__(256, 2) void pw_conv_kernel(const unet_conv_desc d,
         }
       }
     }
-    for (int c = 0; c < nchunks; ++c) {
-      const float sc[8] = {scq[0].x, scq[0].y, scq[0].z, scq[0].w, scq[1].x, scq[1].y, scq[1].z, scq[1].w};
-      const float sf[8] = {sfq[0].x, sfq[0].y, sfq[0].z, sfq[0].w, sfq[1].x, sfq[1].y, sfq[1].z, sfq[1].w};
-      F xb[NB];
+    setup(tile + tstride, xoffn, gokn, gpn);   // the next tile's offsets: its first XD chunks load during this one
+    for (int c0 = 0; c0 < nchunks; c0 += XD) {
 #pragma unroll
-      for (int b = 0; b < NB; ++b) xb[b] = pw_act<T>(xq[b], act, sc, sf, lo, gm[b]);
-      // the next step's operands (the next chunk, or the next tile's first chunk)
-      uint4 xn[NB], wn[NA];
-      float4 scn[2], sfn[2];
-      if (c + 1 < nchunks) {
+      for (int u = 0; u < XD; ++u) {
+        const int c = c0 + u;
+        const float sc[8] = {scq[0].x, scq[0].y, scq[0].z, scq[0].w, scq[1].x, scq[1].y, scq[1].z, scq[1].w};
+        const float sf[8] = {sfq[0].x, sfq[0].y, sfq[0].z, sfq[0].w, sfq[1].x, sfq[1].y, sfq[1].z, sfq[1].w};
+        F xb[NB];
 #pragma unroll
-        for (int b = 0; b < NB; ++b) xn[b] = pw_ld(xr, xoff[b], (unsigned)(c + 1) * 64u);
-        stage(c + 1, wn, scn, sfn);
-      } else {
-        setup(tile + tstride, xn);
-        stage(0, wn, scn, sfn);
+        for (int b = 0; b < NB; ++b) xb[b] = pw_act<T>(xq[u][b], act, sc, sf, lo, gm[b]);
+        // ring slot u: chunk c + XD (of this tile, or of the next one)
+        const int cn = c + XD;
+        if (cn < nchunks) {
+#pragma unroll
+          for (int b = 0; b < NB; ++b) xq[u][b] = pw_ld(xr, xoff[b], (unsigned)cn * 64u);
+        } else {
+#pragma unroll
+          for (int b = 0; b < NB; ++b) xq[u][b] = pw_ld(xr, xoffn[b], (unsigned)(cn - nchunks) * 64u);
+        }
+        // the next step's weights and scale / shift
+        uint4 wn[NA];
+        float4 scn[2], sfn[2];
+        stage(c + 1 < nchunks ? c + 1 : 0, wn, scn, sfn);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          const F wa = __builtin_bit_cast(F, wq[a]);
+#pragma unroll
+          for (int b = 0; b < NB; ++b) acc[a][b] = Mma<T>::mma(wa, xb[b], acc[a][b]);
+        }
+#pragma unroll
+        for (int a = 0; a < NA; ++a) wq[a] = wn[a];
+        scq[0] = scn[0]; scq[1] = scn[1]; sfq[0] = sfn[0]; sfq[1] = sfn[1];
       }
-#pragma unroll
-      for (int a = 0; a < NA; ++a) {
-        const F wa = __builtin_bit_cast(F, wq[a]);
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[a][b] = Mma<T>::mma(wa, xb[b], acc[a][b]);
-      }
-#pragma unroll
-      for (int b = 0; b < NB; ++b) xq[b] = xn[b];
-#pragma unroll
-      for (int a = 0; a < NA; ++a) wq[a] = wn[a];
-      scq[0] = scn[0]; scq[1] = scn[1]; sfq[0] = sfn[0]; sfq[1] = sfn[1];
     }
 
     // epilogue: acc[a][b][r] = out[px = pw0 + 16b + i16][co = co0 + 16a + 4g + r]
@@ -267,6 +280,8 @@ __global__ __launch_bounds__(256, 2) void pw_conv_kernel(const unet_conv_desc d,
         }
       }
     }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) { xoff[b] = xoffn[b]; gok[b] = gokn[b]; gp[b] = gpn[b]; }
   }
   if constexpr (OMK == 0) {
     if (d.stats) {
@@ -598,16 +613,32 @@ int pw_conv_rows(const unet_conv_desc* d) {
   return pw_blocks(d, nb);
 }
 
-template <typename T, int NA, int NB>
-static int launch_pw(const unet_conv_desc* d, hipStream_t st) {
+template <typename T, int NA, int NB, int XD>
+static void launch_pw_xd(const unet_conv_desc* d, hipStream_t st) {
   const long long P = (long long)d->N * d->H * d->W;
   dim3 grid(pw_blocks(d, NB), d->Cout / (16 * NA));
   if (d->out_mode == UNET_OUT_F32_GATED)
-    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 2>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 2, XD>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
   else if (d->out_mode == UNET_OUT_F32)
-    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 1>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 1, XD>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
   else
-    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 0>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+    hipLaunchKernelGGL((pw_conv_kernel<T, NA, NB, 0, XD>), grid, dim3(256), 0, st, *d, P, d->Cin / 32);
+}
+// x prefetch depth: 4 chunks where the chunk count allows (NB = 2: 8 registers per ring slot), else 2 or 1
+// (UNET_PW_XD: A/B cap, read per call)
+template <typename T, int NA, int NB>
+static int launch_pw(const unet_conv_desc* d, hipStream_t st) {
+  const int nch = d->Cin / 32;
+  const char* e = getenv("UNET_PW_XD");
+  const int cap = e ? atoi(e) : 4;
+  if constexpr (NB == 2) {
+    if (cap >= 4 && nch % 4 == 0) {
+      launch_pw_xd<T, NA, NB, 4>(d, st);
+      return check_launch("pw_conv");
+    }
+  }
+  if (cap >= 2 && nch % 2 == 0) launch_pw_xd<T, NA, NB, 2>(d, st);
+  else launch_pw_xd<T, NA, NB, 1>(d, st);
   return check_launch("pw_conv");
 }
 
