@@ -308,7 +308,7 @@ def main():
     # launch (fwd + dgrad; the 32x32x16-MFMA conv5_kernel tiles on the large maps, their 128-output-channel
     # conv5w_kernel form (round 6) where it serves, and the 16x16x32 conv3_kernel tiles on the rest, prefix match)
     tn = {"bf16": "bf16", "fp16": "fp16"}.get(args.precision)
-    family = (f"conv3_kernel<{tn},3,", f"conv5_kernel<{tn},", f"conv5w_kernel<{tn}>") if tn else ("conv2_kernel<fp32,3,",)
+    family = (f"conv3_kernel<{tn},3,", f"conv5_kernel<{tn},", f"conv5w_kernel<{tn}") if tn else ("conv2_kernel<fp32,3,",)
     if args.probe:
         family = (args.probe,)
     target = "|".join(family)

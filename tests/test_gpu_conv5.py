@@ -23,14 +23,20 @@ PATH = {"conv5": {"UNET_CONV5": "1"}}
 
 def _wide(N, H, W, cin, cout, mode="y", src="plain"):
     """conv5w (csrc/conv5w.hip, round 6) serves, by default, the BN-activation forwards with >= 256 input channels
-    and >= 128 output channels whose 16 x 32 x 128 tiles fill the chip (conv5w_ok)"""
-    return (mode == "y" and src != "plain" and cin >= 256 and cout % 128 == 0
-            and N * -(-W // 32) * -(-H // 16) * (cout // 128) >= 256)
+    and >= 128 output channels whose 16 x 32 x 128 tiles (or else 8 x 32 x 128: ",4") fill the chip (conv5w_ok)"""
+    if not (mode == "y" and src != "plain" and cin >= 256 and cout % 128 == 0):
+        return None
+    for mi, suffix in ((8, ""), (4, ",4")):
+        if N * -(-W // 32) * -(-H // (2 * mi)) * (cout // 128) >= 256:
+            return suffix
+    return None
 
 
 def _want(prec, cout, path, shape=None, mode="y", src="plain"):
-    if shape is not None and _wide(shape[0], shape[1], shape[2], shape[3], cout, mode, src):
-        return f"conv5w_kernel<{TN[prec]}>"
+    if shape is not None:
+        w = _wide(shape[0], shape[1], shape[2], shape[3], cout, mode, src)
+        if w is not None:
+            return f"conv5w_kernel<{TN[prec]}{w}>"
     return f"conv5_kernel<{TN[prec]},4>"
 
 

@@ -82,7 +82,7 @@ def main():
         fetch, write = per_kernel(rows_of(d1), "FETCH_SIZE"), per_kernel(rows_of(d2), "WRITE_SIZE")
         fams = dict(HBM_FAMILIES)
         for prec, rx in CONV_FAMILY.items():
-            key = f"conv3_kernel<{prec},3,|conv5_kernel<{prec},|conv5w_kernel<{prec}>"   # bench.py's family key
+            key = f"conv3_kernel<{prec},3,|conv5_kernel<{prec},|conv5w_kernel<{prec}"   # bench.py's family key
             fams[key] = rx
         # every conv5 / conv3 instantiation separately (the conv family's traffic split)
         for k in set(fetch[0]) | set(write[0]):

@@ -37,16 +37,19 @@
 
 namespace unet {
 
-constexpr int W5_MI = 8;                    // wave-tile rows
 constexpr int W5_WM = 2;                    // wave row groups
-constexpr int W5_TH = W5_WM * W5_MI;        // tile rows (16)
 constexpr int W5_W = 32, W5_HW = 34;        // tile / halo width (pixels)
 constexpr int W5_BN = 128;                  // output channels per workgroup (4 quarters of 32)
 constexpr int W5_ROWB = 2 * W5_HW * 16;     // bytes per halo row of an image (1088)
-constexpr int W5_NS = 2 * W5_HW * (W5_TH + 2);   // 16-byte slots per image (1224)
-constexpr int W5_NI = (W5_NS + 63) / 64;    // DMA instructions per image (20)
-constexpr int W5_DPW = (W5_NI + 7) / 8;     // per wave (3)
-constexpr int W5_IMG = W5_NI * 1024;
+// MI: wave-tile rows — 8 (16-row workgroup tiles), or 4 (8-row tiles: twice the tiles, for the 64^2 maps)
+template <int MI>
+struct W5Geo {
+  static constexpr int TH = W5_WM * MI;                 // tile rows
+  static constexpr int NS = 2 * W5_HW * (TH + 2);       // 16-byte slots per image (MI 8: 1224)
+  static constexpr int NI = (NS + 63) / 64;             // DMA instructions per image (20)
+  static constexpr int DPW = (NI + 7) / 8;              // per wave (3)
+  static constexpr int IMG = NI * 1024;
+};
 constexpr int W5_NWF = 9 * 4;               // weight fragments per chunk (9 taps x 4 quarters)
 constexpr int W5_WPW = (W5_NWF + 7) / 8;    // per wave (5; 4 of the 40 go to the junk slot)
 constexpr int W5_WIMG = W5_NWF * 1024;
@@ -55,8 +58,9 @@ constexpr int W5_TABS = W5_CMAX + 8;        // scale / shift table stride (each 
 constexpr int W5_OM_Y = 0, W5_OM_F32 = 1, W5_OM_BNB = 2;
 constexpr int W5_SK_PLAIN1 = 4;             // = conv5.hip's SK5_PLAIN1: one stored source, C % 16 == 0
 
-template <bool ACT, bool GATED, bool BNB>
+template <int MI, bool ACT, bool GATED, bool BNB>
 struct W5Lay {
+  static constexpr int W5_IMG = W5Geo<MI>::IMG, W5_NI = W5Geo<MI>::NI;
   static constexpr int NCOMP = ACT ? 2 : 3;
   static constexpr int OFF_COMP = 0;
   static constexpr int OFF_RAW = OFF_COMP + NCOMP * W5_IMG;
@@ -72,15 +76,16 @@ struct W5Lay {
 // SK: W5_SK_PLAIN1 (stored, one source), SK_ACT (one BN activation, GATE: attention-gated) or SK_ACT_PLAIN
 // (src0 BN activation (+gate), src1 stored: the up-block concat); OM: W5_OM_Y, W5_OM_F32 or W5_OM_BNB (y + the
 // BN-backward sums of the activation whose gradient this dgrad writes; the last two with PLAIN1 only)
-template <typename T, int OM, int SK, int GATE>
+template <typename T, int OM, int SK, int GATE, int MI = 8>
 __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, int tiles_w, int tiles_h, int mtiles,
                                                         int nch, int prio) {
   using F = typename Mma32<T>::frag;
   constexpr bool ACT = SK != W5_SK_PLAIN1;
   constexpr bool ONE = SK != SK_ACT_PLAIN;
   constexpr bool GATED = ACT && GATE;
-  using Lay = W5Lay<ACT, GATED, OM == W5_OM_BNB>;
-  constexpr int MI = W5_MI, TH = W5_TH, NI = W5_NI, DPW = W5_DPW, WPW = W5_WPW, NS = W5_NS;
+  using Lay = W5Lay<MI, ACT, GATED, OM == W5_OM_BNB>;
+  using Geo = W5Geo<MI>;
+  constexpr int TH = Geo::TH, NI = Geo::NI, DPW = Geo::DPW, WPW = W5_WPW, NS = Geo::NS, W5_IMG = Geo::IMG;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[Lay::BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -369,12 +374,13 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
     for (int dy = 0; dy < 3; ++dy) w[0][dy] = *reinterpret_cast<const F*>(wp + (dy * 3) * 4096);
     x[0] = *reinterpret_cast<const F*>(xb + boff[0]);
     x[1] = *reinterpret_cast<const F*>(xb + boff[0] + W5_ROWB);
+    constexpr int R = MI + 2, NSTEP = 3 * R;   // halo rows per tap column, row steps per chunk
 #pragma unroll
-    for (int t = 0; t < 30; ++t) {
-      const int dx = t / 10, r = t % 10;
+    for (int t = 0; t < NSTEP; ++t) {
+      const int dx = t / R, r = t % R;
       // prefetch: the row two steps ahead (possibly the next column's), the next column's weights at rows 2-4
-      if (t + 2 < 30) {
-        const int dx2 = (t + 2) / 10, r2 = (t + 2) % 10;
+      if (t + 2 < NSTEP) {
+        const int dx2 = (t + 2) / R, r2 = (t + 2) % R;
         x[(t + 2) % 3] = *reinterpret_cast<const F*>(xb + boff[dx2] + r2 * W5_ROWB);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
@@ -661,7 +667,15 @@ __global__ __launch_bounds__(512, 1) void conv5w_kernel(const unet_conv_desc d, 
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-static long long w5_mtiles(const unet_conv_desc* d) { return (long long)d->N * cdiv(d->W, W5_W) * cdiv(d->H, W5_TH); }
+static long long w5_mtiles(const unet_conv_desc* d, int mi) {
+  return (long long)d->N * cdiv(d->W, W5_W) * cdiv(d->H, W5_WM * mi);
+}
+// MI of a descriptor: 8 (16-row tiles) where those fill the chip, else 4 (8-row tiles), else none (0)
+static int w5_mi(const unet_conv_desc* d) {
+  if (w5_mtiles(d, 8) * (d->Cout / W5_BN) >= 256) return 8;
+  if (w5_mtiles(d, 4) * (d->Cout / W5_BN) >= 256) return 4;
+  return 0;
+}
 
 // UNET_CONV5W: unset = the measured default (below), 0 = never, 1 = every descriptor it can serve (tests, A/B);
 // read per call so tests can flip it
@@ -710,11 +724,13 @@ bool conv5w_ok(const unet_conv_desc* d) {
   }
   if ((double)d->N * d->H * d->W * 4 >= (double)OOB) return false;
   if ((double)d->N * d->H * d->W * d->Cout * 2 >= (double)OOB) return false;
-  return w5_mtiles(d) * (d->Cout / W5_BN) >= 256;    // enough 16 x 32 x 128 tiles to fill the chip
+  // enough 16 x 32 x 128 tiles to fill the chip, or (BN-activation y outputs only) 8 x 32 x 128 ones
+  const int mi = w5_mi(d);
+  return mi == 8 || (mi == 4 && d->out_mode == UNET_OUT_Y && !d->bnb_stats && s0.kind == UNET_SRC_ACT);
 }
 
 static int w5_gx(const unet_conv_desc* d) {
-  const long long mt = w5_mtiles(d);
+  const long long mt = w5_mtiles(d, w5_mi(d));
   long long gx = cdiv(256, d->Cout / W5_BN);   // one 8-wave workgroup per CU (LDS), persistent
   if (gx > mt) gx = mt;
   return (int)(gx < 1 ? 1 : gx);
@@ -723,17 +739,21 @@ static int w5_gx(const unet_conv_desc* d) {
 int conv5w_stats_rows(const unet_conv_desc* d) { return w5_gx(d) * W5_WM; }
 
 int conv5w_variant(const unet_conv_desc* d, char* buf, int len) {
-  snprintf(buf, len, "conv5w_kernel<%s>", d->dtype == UNET_F16 ? "fp16" : "bf16");
+  if (w5_mi(d) == 4) snprintf(buf, len, "conv5w_kernel<%s,4>", d->dtype == UNET_F16 ? "fp16" : "bf16");
+  else snprintf(buf, len, "conv5w_kernel<%s>", d->dtype == UNET_F16 ? "fp16" : "bf16");
   return 0;
 }
 
-template <typename T, int OM, int SK, int GATE>
+template <typename T, int OM, int SK, int GATE, int MI = 8>
 static int launch5w(const unet_conv_desc* d, int prio, hipStream_t st) {
-  const int tw = cdiv(d->W, W5_W), th = cdiv(d->H, W5_TH);
+  if constexpr (MI == 8 && OM == W5_OM_Y && SK != W5_SK_PLAIN1) {
+    if (w5_mi(d) == 4) return launch5w<T, OM, SK, GATE, 4>(d, prio, st);
+  }
+  const int tw = cdiv(d->W, W5_W), th = cdiv(d->H, W5_WM * MI);
   const int mt = d->N * tw * th;
   const int gy = d->Cout / W5_BN, gx = w5_gx(d);
   const int nch = d->Cin / 16;
-  hipLaunchKernelGGL((conv5w_kernel<T, OM, SK, GATE>), dim3(gx, gy), dim3(512), 0, st, *d, tw, th, mt, nch, prio);
+  hipLaunchKernelGGL((conv5w_kernel<T, OM, SK, GATE, MI>), dim3(gx, gy), dim3(512), 0, st, *d, tw, th, mt, nch, prio);
   return check_launch("conv5w");
 }
 
