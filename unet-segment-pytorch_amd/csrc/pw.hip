@@ -570,14 +570,15 @@ static bool pw_src_ok(const unet_src& s, int C) {
   return (s.kind == UNET_SRC_PLAIN || s.kind == UNET_SRC_ACT) && s.C == C && !(s.gate_p && s.kind != UNET_SRC_ACT);
 }
 
-// the large-pixel-count 1x1 cases (attention-gate projections at 128^2..512^2); smaller maps keep the
-// tiled conv2 / wgrad2 paths, which re-use weights across more pixels per workgroup
+// the 1x1 convs of the attention-gate projections at 64^2..512^2 (P >= 16384 pixels at bs 4).  Round 6: the 64^2
+// ones moved here from the tiled conv2 (the x prefetch ring made the difference: 33 -> 23 us fwd, 37 -> 28 us
+// dgrad, profiles/r06_layerprof_pw_*.txt); UNET_PW_WIDE=0 restores the round-5 cut (P >= 32768, Cin <= 256)
 bool pw_conv_ok(const unet_conv_desc* d) {
   const long long P = (long long)d->N * d->H * d->W;
   if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 1 || d->nsrc != 1 ||
       !pw_src_ok(d->src[0], d->Cin))
     return false;
-  static const int wide = [] { const char* e = getenv("UNET_PW_WIDE"); return e ? atoi(e) : 0; }();
+  static const int wide = [] { const char* e = getenv("UNET_PW_WIDE"); return e ? atoi(e) : 1; }();
   if (d->Cin % 32 || d->Cout % 16) return false;
   if (wide ? (d->Cin > 512 || P < 16384) : (d->Cin > 256 || P < 32768)) return false;
   if (d->out_mode == UNET_OUT_F32) { if (d->split % 4) return false; }
