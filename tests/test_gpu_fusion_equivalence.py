@@ -53,8 +53,8 @@ def _grads(model, x, t, env, seen=None):
 @pytest.mark.parametrize("size", [128, 98])
 def test_fused_backward_bit_identical(prec, size):
     """base 64 at 2 x 128^2: the top gate's W_x dgrad (32 -> 64 channels, 32768 pixels) runs on the 1x1
-    kernel that serves the gated epilogue; 98^2 has odd pooled maps below 49^2 (last row / column without
-    a window)."""
+    kernel that serves the gated epilogue (at 98^2 too since round 6: 19208 pixels); 98^2 has odd pooled maps
+    below 49^2 (last row / column without a window)."""
     from unet.models import AttentionUNet
     torch.manual_seed(3)
     m = AttentionUNet(1, 2, base_features=64).cuda().train()
@@ -68,7 +68,8 @@ def test_fused_backward_bit_identical(prec, size):
     m.load_state_dict(state)   # the same BN running statistics going in
     out1, g1 = _grads(m, x, t, {"UNET_NO_POOL_FOLD": "1", "UNET_NO_GATE_FUSE": "1"}, seen1)
     assert "unet_bn_bwd_reduce_pool" in seen0 and "unet_bn_bwd_reduce_pool" not in seen1
-    assert ("unet_conv:4" in seen0) == (prec != "fp32" and size == 128), sorted(seen0)
+    # the gated W_x dgrad runs on the 1x1 kernel from 16384 pixels (csrc/pw.hip pw_conv_ok; 32768 before round 6)
+    assert ("unet_conv:4" in seen0) == (prec != "fp32" and 2 * size * size >= 16384), sorted(seen0)
     assert "unet_conv:4" not in seen1 and "unet_conv:2" in seen1
     assert torch.equal(out0, out1)
     diff = [n for n in g0 if not torch.equal(g0[n], g1[n])]

@@ -346,31 +346,42 @@ __global__ void outconv_fwd_vec_kernel(long long P, int HW, int C, int G, const 
     for (int k = 0; k < KT; ++k) wk[k][j] = w[k * C + c0 + j];
   }
   const long long stride = (long long)gridDim.x * nw * ppw;
-  for (long long q = ((long long)blockIdx.x * nw + wave) * ppw + lane / G; q < P; q += stride) {
-    float a[8];
-    if constexpr (sizeof(T) == 2) {
-      load_vec<T>(y + q * C + c0, a);
-    } else {
-      load_vec<float>((const float*)y + q * C + c0, a);
-      load_vec<float>((const float*)y + q * C + c0 + 4, a + 4);
-    }
-    float acc[KT];
+  // OC_U pixels per trip, all their loads issued first (round 6: one memory round trip per trip instead of per
+  // pixel; 2.5 TB/s before); each pixel's sum is unchanged
+  constexpr int OC_U = 4;
+  for (long long q = ((long long)blockIdx.x * nw + wave) * ppw + lane / G; q < P; q += OC_U * stride) {
+    float a[OC_U][8];
 #pragma unroll
-    for (int k = 0; k < KT; ++k) acc[k] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = a[j] * s[j] + f[j];
-      if (relu) v = fmaxf(v, 0.f);
-#pragma unroll
-      for (int k = 0; k < KT; ++k) acc[k] += wk[k][j] * v;
+    for (int u = 0; u < OC_U; ++u) {
+      const long long qq = q + u * stride < P ? q + u * stride : q;
+      if constexpr (sizeof(T) == 2) {
+        load_vec<T>(y + qq * C + c0, a[u]);
+      } else {
+        load_vec<float>((const float*)y + qq * C + c0, a[u]);
+        load_vec<float>((const float*)y + qq * C + c0 + 4, a[u] + 4);
+      }
     }
 #pragma unroll
-    for (int k = 0; k < KT; ++k)
-      for (int o = G >> 1; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, 64);
-    if (sub == 0) {
-      const long long n = q / HW, hw = q % HW;
+    for (int u = 0; u < OC_U; ++u) {
+      const long long qu = q + u * stride;
+      float acc[KT];
 #pragma unroll
-      for (int k = 0; k < KT; ++k) out[(n * KT + k) * HW + hw] = acc[k] + b[k];
+      for (int k = 0; k < KT; ++k) acc[k] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = a[u][j] * s[j] + f[j];
+        if (relu) v = fmaxf(v, 0.f);
+#pragma unroll
+        for (int k = 0; k < KT; ++k) acc[k] += wk[k][j] * v;
+      }
+#pragma unroll
+      for (int k = 0; k < KT; ++k)
+        for (int o = G >> 1; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+      if (sub == 0 && qu < P) {
+        const long long n = qu / HW, hw = qu % HW;
+#pragma unroll
+        for (int k = 0; k < KT; ++k) out[(n * KT + k) * HW + hw] = acc[k] + b[k];
+      }
     }
   }
 }
@@ -548,24 +559,37 @@ __global__ __launch_bounds__(256) void outconv_bwd_bn_kernel(long long P, int HW
   const float lo = relu ? 0.f : -INFINITY;
   const long long per = (P + gridDim.x - 1) / gridDim.x;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  for (long long q = p0 + py; q < p1; q += R) {
-    const long long n = q / HW, hw = q % HW;
-    float dlk[KK];
+  // OB_U pixels per trip, loads first (round 6); the sums still run over q, q + R, ... in order (bit-identical)
+  constexpr int OB_U = 4;
+  for (long long q = p0 + py; q < p1; q += OB_U * R) {
+    float dlu[OB_U][KK], yu[OB_U][8];
 #pragma unroll
-    for (int k = 0; k < KK; ++k) { dlk[k] = dl[(n * KK + k) * HW + hw]; db[k] += dlk[k]; }
-    float yv[8];
-    load_vec<T>(y + q * C + c0, yv);
-    if constexpr (sizeof(T) == 4) load_vec<T>(y + q * C + c0 + 4, yv + 4);
+    for (int u = 0; u < OB_U; ++u) {
+      const long long qq = q + u * R < p1 ? q + u * R : q;
+      const long long n = qq / HW, hw = qq % HW;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float pre = yv[j] * s8[j] + f8[j];
-      const float a = fmaxf(pre, lo);
-      float g = 0.f;
+      for (int k = 0; k < KK; ++k) dlu[u][k] = dl[(n * KK + k) * HW + hw];
+      load_vec<T>(y + qq * C + c0, yu[u]);
+      if constexpr (sizeof(T) == 4) load_vec<T>(y + qq * C + c0 + 4, yu[u] + 4);
+    }
 #pragma unroll
-      for (int k = 0; k < KK; ++k) { g += wk[k][j] * dlk[k]; dw[k][j] += dlk[k] * a; }
-      const float gm = (relu && !(pre > 0.f)) ? 0.f : g;
-      sg[j] += gm;
-      sgx[j] += gm * (yv[j] - mu[j]) * is[j];
+    for (int u = 0; u < OB_U; ++u) {
+      if (q + u * R >= p1) break;
+      const float* dlk = dlu[u];
+      const float* yv = yu[u];
+#pragma unroll
+      for (int k = 0; k < KK; ++k) db[k] += dlk[k];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pre = yv[j] * s8[j] + f8[j];
+        const float a = fmaxf(pre, lo);
+        float g = 0.f;
+#pragma unroll
+        for (int k = 0; k < KK; ++k) { g += wk[k][j] * dlk[k]; dw[k][j] += dlk[k] * a; }
+        const float gm = (relu && !(pre > 0.f)) ? 0.f : g;
+        sg[j] += gm;
+        sgx[j] += gm * (yv[j] - mu[j]) * is[j];
+      }
     }
   }
 #pragma unroll
@@ -623,25 +647,38 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_oc_kernel(long long P, int H
     for (int k = 0; k < KK; ++k) wk[k][j] = w[k * C + c];
   }
   const int cvs = __builtin_ctz(CV);
-  for (; e < total; e += stride) {
-    const long long p = e >> cvs;
-    const unsigned n = (unsigned)p / (unsigned)HW, hw = (unsigned)p - n * (unsigned)HW;
-    float dlk[KK];
+  // AO_U elements per trip, every load before the stores (dy may alias the loads as far as the compiler knows,
+  // which serialised one memory round trip per pixel; round 6); elementwise, results unchanged
+  constexpr int AO_U = 4;
+  for (; e < total; e += AO_U * stride) {
+    float dlu[AO_U][KK], yu[AO_U][8];
+    long long pu[AO_U];
 #pragma unroll
-    for (int k = 0; k < KK; ++k) dlk[k] = dl[((size_t)n * KK + k) * HW + hw];
-    float yv[8], o[8];
-    load_vec<T>(y + p * C + cv * 8, yv);
-    if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yv + 4);
+    for (int u = 0; u < AO_U; ++u) {
+      const long long p = (e + u * stride < total ? e + u * stride : e) >> cvs;
+      pu[u] = p;
+      const unsigned n = (unsigned)p / (unsigned)HW, hw = (unsigned)p - n * (unsigned)HW;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float g = 0.f;
-#pragma unroll
-      for (int k = 0; k < KK; ++k) g += wk[k][j] * dlk[k];
-      const float gj = (relu && !(yv[j] * sc[j] + sf[j] > 0.f)) ? 0.f : g;
-      o[j] = A[j] * gj + B[j] * yv[j] + Cc[j];
+      for (int k = 0; k < KK; ++k) dlu[u][k] = dl[((size_t)n * KK + k) * HW + hw];
+      load_vec<T>(y + p * C + cv * 8, yu[u]);
+      if constexpr (sizeof(T) == 4) load_vec<T>(y + p * C + cv * 8 + 4, yu[u] + 4);
     }
-    store_vec<T>(dy + p * C + cv * 8, o);
-    if constexpr (sizeof(T) == 4) store_vec<T>(dy + p * C + cv * 8 + 4, o + 4);
+#pragma unroll
+    for (int u = 0; u < AO_U; ++u) {
+      if (e + u * stride >= total) break;
+      const long long p = pu[u];
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float g = 0.f;
+#pragma unroll
+        for (int k = 0; k < KK; ++k) g += wk[k][j] * dlu[u][k];
+        const float gj = (relu && !(yu[u][j] * sc[j] + sf[j] > 0.f)) ? 0.f : g;
+        o[j] = A[j] * gj + B[j] * yu[u][j] + Cc[j];
+      }
+      store_vec<T>(dy + p * C + cv * 8, o);
+      if constexpr (sizeof(T) == 4) store_vec<T>(dy + p * C + cv * 8 + 4, o + 4);
+    }
   }
 }
 
