@@ -184,7 +184,7 @@ __global__ void bn_bwd_reduce_kernel(long long P, int C, int CL, const G* da, co
     for (long long p = p0 + py; p < p1; p += R) {
       const float yv = to_f(y[p * C + c]);
       float g = to_f(da[p * C + c]);
-      if (relu && !(yv * sc + sf > 0.f)) g = 0.f;
+      if (relu && !(__builtin_fmaf(yv, sc, sf) > 0.f)) g = 0.f;
       sg += g;
       sgx += g * (yv - mu) * is;
     }
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_vec_kernel(long long P, int
         if (!ok[u]) continue;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float gj = (relu && !(yv[u][j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[u][j];
+          const float gj = (relu && !(__builtin_fmaf(yv[u][j], sc[j], sf[j]) > 0.f)) ? 0.f : g[u][j];
           sg[j] += gj;
           sgx[j] += gj * (yv[u][j] - mu[j]) * is[j];
         }
@@ -398,8 +398,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_vec_kernel(long long P, int 
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float gj = (relu && !(yv[u][j] * sc[j] + sf[j] > 0.f)) ? 0.f : g[u][j];
-        o[j] = A[j] * gj + B[j] * yv[u][j] + Cc[j];
+        const float gj = (relu && !(__builtin_fmaf(yv[u][j], sc[j], sf[j]) > 0.f)) ? 0.f : g[u][j];
+        // explicit fma order, here and in the pre-activation y * scale + shift of the ReLU masks (the compiler's
+        // contraction choice moved with the code's shape in round 6: fused and unfused paths must round alike);
+        // the OutConv and attention-gate forms (misc.hip, gate.hip) round the same way
+        o[j] = f32_rounded(__builtin_fmaf(A[j], gj, __builtin_fmaf(B[j], yv[u][j], Cc[j])));
       }
       if constexpr (sizeof(T) == 2) {
         store_vec<T>(dy + p * C + cv * 8, o);
@@ -518,8 +521,8 @@ __global__ void bn_bwd_apply_kernel(long long P, int C, int CL, const G* da, con
   for (long long p = p0 + py; p < p1; p += R) {
     const float yv = to_f(y[p * C + c]);
     float g = to_f(da[p * C + c]);
-    if (relu && !(yv * sc + sf > 0.f)) g = 0.f;
-    dy[p * C + c] = from_f<T>(A * g + B * yv + Cc);
+    if (relu && !(__builtin_fmaf(yv, sc, sf) > 0.f)) g = 0.f;
+    dy[p * C + c] = from_f<T>(f32_rounded(__builtin_fmaf(A, g, __builtin_fmaf(B, yv, Cc))));
   }
 }
 

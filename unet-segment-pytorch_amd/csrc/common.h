@@ -40,6 +40,15 @@ template <> __device__ __forceinline__ float from_f<float>(float x) { return x; 
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
 template <> __device__ __forceinline__ f16 from_f<f16>(float x) { return (f16)x; }
 
+// an fp32 result the compiler may not fold into the 16-bit conversion that follows: fptrunc(fma) contracts to
+// v_fma_mix{lo,hi}_f16 (the exact fma rounded once, straight to 16 bits) wherever the instruction selector finds the
+// pattern, so two instantiations of one expression could round an element differently (round 6: the pooled and
+// plain BN-backward applies); behind this, every path rounds to fp32 first, then to the storage type
+__device__ __forceinline__ float f32_rounded(float x) {
+  __asm__("" : "+v"(x));
+  return x;
+}
+
 // load VEC elements (16 B aligned) into floats
 template <typename T> __device__ __forceinline__ void load_vec(const T* p, float* v);
 template <> __device__ __forceinline__ void load_vec<float>(const float* p, float* v) {

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(NTHR) void conv_generic_kernel(const unet_conv_desc
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const long long sp = (n * ps.H + 2 * oh + (q >> 1)) * (long long)ps.W + 2 * ow + (q & 1);
-              float a = to_f(ysrc[sp * d.Cout + co]) * sc + sf;
+              float a = __builtin_fmaf(to_f(ysrc[sp * d.Cout + co]), sc, sf);
               if (ps.relu) a = fmaxf(a, 0.f);
               if (a > best || a != a) { best = a; bq = q; }
             }

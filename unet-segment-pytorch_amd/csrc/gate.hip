@@ -90,7 +90,7 @@ __global__ void gate_bwd1_kernel(long long P, int Cx, const float* dxs, const T*
     float* o = dx ? dx + q * Cx : nullptr;
     float ds = 0.f;
     for (int c = 0; c < Cx; ++c) {
-      float xv = to_f(y[c]) * sx[c] + bx[c];
+      float xv = __builtin_fmaf(to_f(y[c]), sx[c], bx[c]);
       if (relu) xv = fmaxf(xv, 0.f);
       const float dv = d[c];
       ds += dv * xv;
@@ -224,7 +224,7 @@ __global__ void gate_bwd1_vec_kernel(long long P, int Cx, int G, const float* __
       float ds = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float xv = y[u][j] * sc[j] + sf[j];
+        float xv = __builtin_fmaf(y[u][j], sc[j], sf[j]);
         if (relu) xv = fmaxf(xv, 0.f);
         ds += d[u][j] * xv;
       }
@@ -329,8 +329,8 @@ __global__ void gate_bwd3_kernel(long long P, int Ci, int CL, const T* gw, const
     const float a = fmaxf(g * gs + gb + x * xs + xb, 0.f);
     const float dp = A * dq[q] + B * pp[q] + Cc;
     const float dz = a > 0.f ? dp * w : 0.f;
-    dgw[q * Ci + c] = from_f<T>(gA * dz + gB * g + gC);
-    dxw[q * Ci + c] = from_f<T>(xA * dz + xB * x + xC);
+    dgw[q * Ci + c] = from_f<T>(f32_rounded(__builtin_fmaf(gA, dz, __builtin_fmaf(gB, g, gC))));   // bn.hip's rounding
+    dxw[q * Ci + c] = from_f<T>(f32_rounded(__builtin_fmaf(xA, dz, __builtin_fmaf(xB, x, xC))));
   }
 }
 
@@ -460,8 +460,8 @@ __global__ __launch_bounds__(256) void gate_bwd3_vec_kernel(long long P, int Ci,
       for (int j = 0; j < 8; ++j) {
         const float a = fmaxf(g[u][j] * gs[j] + gb[j] + x[u][j] * xs[j] + xb[j], 0.f);
         const float dz = a > 0.f ? dp * w[j] : 0.f;
-        og[j] = gA[j] * dz + gB[j] * g[u][j] + gC[j];
-        ox[j] = xA[j] * dz + xB[j] * x[u][j] + xC[j];
+        og[j] = f32_rounded(__builtin_fmaf(gA[j], dz, __builtin_fmaf(gB[j], g[u][j], gC[j])));   // bn.hip's rounding
+        ox[j] = f32_rounded(__builtin_fmaf(xA[j], dz, __builtin_fmaf(xB[j], x[u][j], xC[j])));
       }
       store8<T>(dgw + qq * Ci + c0, og);
       store8<T>(dxw + qq * Ci + c0, ox);

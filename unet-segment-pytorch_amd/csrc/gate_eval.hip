@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void gate_eval_kernel(const GateEvalArgs a) {
         float v[8];
         unpack8_16<T>(q[b], v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = ok[b] ? fmaxf(v[j] * sc[j] + sf[j], lo) : 0.f;
+        for (int j = 0; j < 8; ++j) v[j] = ok[b] ? fmaxf(__builtin_fmaf(v[j], sc[j], sf[j]), lo) : 0.f;
         v4[b] = pack8_16<T>(v);
       }
 #pragma unroll

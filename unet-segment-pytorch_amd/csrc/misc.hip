@@ -317,7 +317,7 @@ __global__ void outconv_fwd_kernel(long long P, int HW, int C, int K, const T* y
     for (int k = 0; k < OC_MAXK; ++k) acc[k] = (k < K) ? b[k] : 0.f;
     const T* yp = y + q * C;
     for (int c = 0; c < C; ++c) {
-      float a = to_f(yp[c]) * s_sc[c] + s_sf[c];
+      float a = __builtin_fmaf(to_f(yp[c]), s_sc[c], s_sf[c]);
       if (relu) a = fmaxf(a, 0.f);
 #pragma unroll
       for (int k = 0; k < OC_MAXK; ++k)
@@ -369,7 +369,7 @@ __global__ void outconv_fwd_vec_kernel(long long P, int HW, int C, int G, const 
       for (int k = 0; k < KT; ++k) acc[k] = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float v = a[u][j] * s[j] + f[j];
+        float v = __builtin_fmaf(a[u][j], s[j], f[j]);
         if (relu) v = fmaxf(v, 0.f);
 #pragma unroll
         for (int k = 0; k < KT; ++k) acc[k] += wk[k][j] * v;
@@ -412,7 +412,7 @@ __global__ void outconv_bwd_kernel(long long P, int HW, int C, int CL, int K, co
       db[k] += dlk[k];
     }
     if (c < C) {
-      float a = to_f(y[q * C + c]) * s + f;
+      float a = __builtin_fmaf(to_f(y[q * C + c]), s, f);
       if (relu) a = fmaxf(a, 0.f);
 #pragma unroll
       for (int k = 0; k < OC_MAXK; ++k) dw[k] += dlk[k] * a;
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(256) void outconv_bwd_vec_kernel(long long P, int H
     float g[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      a[j] = fmaxf(a[j] * s8[j] + f8[j], lo);
+      a[j] = fmaxf(__builtin_fmaf(a[j], s8[j], f8[j]), lo);
       g[j] = 0.f;
 #pragma unroll
       for (int k = 0; k < KK; ++k) { g[j] += wk[k][j] * dlk[k]; dw[k][j] += dlk[k] * a[j]; }
@@ -581,7 +581,7 @@ __global__ __launch_bounds__(256) void outconv_bwd_bn_kernel(long long P, int HW
       for (int k = 0; k < KK; ++k) db[k] += dlk[k];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float pre = yv[j] * s8[j] + f8[j];
+        const float pre = __builtin_fmaf(yv[j], s8[j], f8[j]);
         const float a = fmaxf(pre, lo);
         float g = 0.f;
 #pragma unroll
@@ -648,7 +648,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_oc_kernel(long long P, int H
   }
   const int cvs = __builtin_ctz(CV);
   // AO_U elements per trip, every load before the stores (dy may alias the loads as far as the compiler knows,
-  // which serialised one memory round trip per pixel; round 6); elementwise, results unchanged
+  // which serialised one memory round trip per pixel; round 6); elementwise.  The unroll moved the compiler's
+  // fma contraction of o = A g + B y + C (last bits of dy); the order is now explicit, as in bn.hip
   constexpr int AO_U = 4;
   for (; e < total; e += AO_U * stride) {
     float dlu[AO_U][KK], yu[AO_U][8];
@@ -673,8 +674,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_oc_kernel(long long P, int H
         float g = 0.f;
 #pragma unroll
         for (int k = 0; k < KK; ++k) g += wk[k][j] * dlu[u][k];
-        const float gj = (relu && !(yu[u][j] * sc[j] + sf[j] > 0.f)) ? 0.f : g;
-        o[j] = A[j] * gj + B[j] * yu[u][j] + Cc[j];
+        const float gj = (relu && !(__builtin_fmaf(yu[u][j], sc[j], sf[j]) > 0.f)) ? 0.f : g;
+        o[j] = f32_rounded(__builtin_fmaf(A[j], gj, __builtin_fmaf(B[j], yu[u][j], Cc[j])));   // bn.hip's rounding
       }
       store_vec<T>(dy + p * C + cv * 8, o);
       if constexpr (sizeof(T) == 4) store_vec<T>(dy + p * C + cv * 8 + 4, o + 4);
@@ -752,7 +753,7 @@ __global__ void nhwc_to_nchw_kernel(long long N, int C, int H, int W, const T* x
     const int c = t % C;
     const long long n = t / C;
     float v = to_f(x[(n * HW + hw) * C + c]);
-    if (sc) v = v * sc[c] + sf[c];
+    if (sc) v = __builtin_fmaf(v, sc[c], sf[c]);
     if (relu) v = fmaxf(v, 0.f);
     y[e] = v;
   }
@@ -768,7 +769,7 @@ __global__ void gated_to_nchw_kernel(long long N, int C, int H, int W, const T* 
     const long long t = e / HW;
     const int c = t % C;
     const long long n = t / C;
-    float v = to_f(x[(n * HW + hw) * C + c]) * sc[c] + sf[c];
+    float v = __builtin_fmaf(to_f(x[(n * HW + hw) * C + c]), sc[c], sf[c]);
     if (relu) v = fmaxf(v, 0.f);
     y[e] = v * sigmoidf_(p[n * HW + hw] * ab[0] + ab[1]);
   }
@@ -1020,7 +1021,7 @@ __global__ void materialize_pool_kernel(const unet_src s, long long N, int H, in
       load_vec<T>((const T*)s.data + (((n * s.H + 2 * y + (q >> 1)) * (long long)s.W + 2 * x + (q & 1)) * C + cv * VEC), v);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
-        const float a = fmaxf(v[j] * sc[j] + sf[j], lo);
+        const float a = fmaxf(__builtin_fmaf(v[j], sc[j], sf[j]), lo);
         if (q == 0 || a > best[j] || a != a) { best[j] = a; arg[j] = q; }
       }
     }

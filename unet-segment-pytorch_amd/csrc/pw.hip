@@ -38,7 +38,7 @@ __device__ __forceinline__ typename Mma<T>::frag pw_act(uint4 q, bool act, const
   unpack8_16<T>(q, v);
   if (act) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sf[j], lo);
+    for (int j = 0; j < 8; ++j) v[j] = fmaxf(__builtin_fmaf(v[j], sc[j], sf[j]), lo);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] *= gmul;

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(64 * WCO * WCI) void wgrad2_kernel(const unet_wgrad
           const float lo = sv.relu ? 0.f : -INFINITY;
           const float gm = sv.gate_p ? sigmoidf_(xg[k] * sv.gate_ab[0] + sv.gate_ab[1]) : 1.f;
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) v[j] = inb ? fmaxf(v[j] * sc[j] + sf[j], lo) * gm : 0.f;
+          for (int j = 0; j < VEC; ++j) v[j] = inb ? fmaxf(__builtin_fmaf(v[j], sc[j], sf[j]), lo) * gm : 0.f;
           o = pack8_16<T>(v);
         }
         *reinterpret_cast<uint4*>(buf + hp * RSX + vx * VEC) = o;
