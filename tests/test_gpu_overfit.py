@@ -88,10 +88,11 @@ ALPHA = 0.01      # the ensemble gate's false-alarm rate per test
 BOUND_CAP = 5e-3   # the member-0 |HIP - fp64| ceiling (a fixed cap, not a bound measured in the run)
 
 
-def _report(msg):
-    """printed, and echoed on the process's real stderr so the suite's log keeps it for a passing test too"""
+def _report(request, msg):
+    """printed, and echoed with pytest's capture suspended so the suite's log keeps it for a passing test too"""
     print(msg)
-    print(msg, file=sys.__stderr__, flush=True)
+    with _uncaptured(request):
+        print(msg, file=sys.__stderr__, flush=True)
 
 
 def _uncaptured(request):
@@ -155,7 +156,7 @@ def _iqr(v):
     return float(q[1] - q[0])
 
 
-def test_overfit_c1_full_protocol_final_dice(c1, c1_full, c1_ens):
+def test_overfit_c1_full_protocol_final_dice(c1, c1_full, c1_ens, request):
     """The reference's whole protocol (200 epochs, overfit_test.py:69) and its statistic, the last epoch's
     Tumor-Dice (overfit_test.py:218,288), from the seeded weights (member 0) against the fp64 oracle started from
     the SAME weights.  The loop is chaotic: the reference's own fp32 executions from one-ulp
@@ -172,7 +173,7 @@ def test_overfit_c1_full_protocol_final_dice(c1, c1_full, c1_ens):
     d64 = abs(last - r64[-1][1])
     spread = abs(r320[-1][1] - r64[-1][1])
     lo32 = min(r[-1][1] for r in r32)
-    _report(f"[overfit] member 0 last epoch: HIP {last:.6f}, reference fp32 {r320[-1][1]:.6f}, fp64 {r64[-1][1]:.6f}; "
+    _report(request, f"[overfit] member 0 last epoch: HIP {last:.6f}, reference fp32 {r320[-1][1]:.6f}, fp64 {r64[-1][1]:.6f}; "
             f"|HIP - fp64| {d64:.2e} (north_star 1e-3, asserted <= {BOUND_CAP:g}); the reference's own |fp32 - fp64| "
             f"on this start {spread:.2e}; reference fp32 ensemble min {lo32:.6f}")
     assert d64 <= BOUND_CAP, (last, r64[-1][1])
@@ -194,7 +195,7 @@ def _perm_p_median(a, b):
     return hit / tot
 
 
-def test_overfit_c1_ensemble_vs_reference(c1, c1_ens):
+def test_overfit_c1_ensemble_vs_reference(c1, c1_ens, request):
     """The statistic's distribution under rounding noise: K_ENS members each of HIP and
     of the reference fp32, member k of both from the same one-ulp-perturbed start.  A fixed +-1e-3 band on the
     medians is not a test at this K: the members are samples of a chaotic loop, and a rounding-only
@@ -211,14 +212,14 @@ def test_overfit_c1_ensemble_vs_reference(c1, c1_ens):
     l32 = [r[-1][1] for r in r32]
     mh = [sum(e[1] for e in h[-10:]) / 10 for h in hip]
     m32 = [sum(e[1] for e in r[-10:]) / 10 for r in r32]
-    _report("\n[overfit] member: last-epoch dice HIP ref32 | mean of last 10 HIP ref32")
+    _report(request, "\n[overfit] member: last-epoch dice HIP ref32 | mean of last 10 HIP ref32")
     for k in range(K_ENS):
-        _report(f"[overfit] {k}: {lh[k]:.6f} {l32[k]:.6f} | {mh[k]:.6f} {m32[k]:.6f}")
+        _report(request, f"[overfit] {k}: {lh[k]:.6f} {l32[k]:.6f} | {mh[k]:.6f} {m32[k]:.6f}")
     dmed = abs(_median(lh) - _median(l32))
     p_med = _perm_p_median(lh, l32)
     ch, c32 = sum(m < COLLAPSE for m in mh), sum(m < COLLAPSE for m in m32)
     p_col = fisher_exact([[ch, K_ENS - ch], [c32, K_ENS - c32]], alternative="greater").pvalue
-    _report(f"[overfit] median last-epoch dice: HIP {_median(lh):.6f}, ref32 {_median(l32):.6f}; |diff| {dmed:.2e} (north_star "
+    _report(request, f"[overfit] median last-epoch dice: HIP {_median(lh):.6f}, ref32 {_median(l32):.6f}; |diff| {dmed:.2e} (north_star "
           f"1e-3; ref32 IQR {_iqr(l32):.2e}), permutation p {p_med:.3f}; members with mean-of-last-10 < {COLLAPSE}: "
           f"HIP {ch}, ref32 {c32}, Fisher p {p_col:.3f}; asserted p >= {ALPHA}")
     assert p_med >= ALPHA, (dmed, p_med)
