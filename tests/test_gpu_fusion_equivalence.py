@@ -12,7 +12,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _grads(model, x, t, env, seen=None):
+def _grads(model, x, t, env, seen=None, split=False):
     from unet._hip import lib as L
     from unet.utils.loss import DiceBCELoss
     old = {k: os.environ.get(k) for k in ("UNET_NO_POOL_FOLD", "UNET_NO_GATE_FUSE", "UNET_NO_ACT_OUT", "UNET_NO_OC_FUSE",
@@ -22,6 +22,8 @@ def _grads(model, x, t, env, seen=None):
     def rec(name, *args):
         if seen is not None:
             seen.add(name if name != "unet_conv" else f"unet_conv:{args[0].out_mode}")
+            if name == "unet_conv" and args[0].workspace:
+                seen.add("splitk")
             if name == "unet_conv_wgrad" and args[0].ksize == 3:
                 seen.add(f"wgrad3:src0kind={args[0].src[0].kind}")
         return orig(name, *args)
@@ -33,7 +35,8 @@ def _grads(model, x, t, env, seen=None):
         # split-K (round 5) sums a small-map conv's reduction in a different order; the pooled dgrad of the fused
         # path is one of them and the pool-routing epilogue of the unfused path is not, so both runs here keep the
         # unsplit form: what these tests compare is where the fusions add, not the conv's summation order
-        os.environ["UNET_CONV5_SPLIT"] = "0"
+        if not split:
+            os.environ["UNET_CONV5_SPLIT"] = "0"
         os.environ.update(env)
         model.zero_grad(set_to_none=True)
         out = model(x)
@@ -74,6 +77,43 @@ def test_fused_backward_bit_identical(prec, size):
     assert torch.equal(out0, out1)
     diff = [n for n in g0 if not torch.equal(g0[n], g1[n])]
     assert not diff, diff
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_fusions_with_splitk_on(prec):
+    """The production configuration: split-K on for the small maps in both runs.  The gate
+    fusion (the x*s term added by the W_x dgrad) does not touch a split conv, so its gradients stay bit-identical
+    with split-K on; the pool fold does — the fused path's pooled dgrad is a split-K conv, the unfused path's
+    pool-routing epilogue is not split — so there the same sums in another order, equal up to the 16-bit
+    roundings such a reorder flips downstream (gated as test_outconv_bn_backward_fused's 16-bit case)."""
+    from unet.models import AttentionUNet
+    torch.manual_seed(3)
+    m = AttentionUNet(1, 2, base_features=64).cuda().train()
+    m.hip_precision = prec
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(2, 1, 128, 128, generator=g) * 2 - 1).cuda()
+    t = (torch.rand(2, 128, 128, generator=g) < 0.1).long().cuda()
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    seen0, seen1, seen2 = set(), set(), set()
+    out0, g0 = _grads(m, x, t, {}, seen0, split=True)
+    m.load_state_dict(state)
+    out1, g1 = _grads(m, x, t, {"UNET_NO_GATE_FUSE": "1"}, seen1, split=True)
+    m.load_state_dict(state)
+    out2, g2 = _grads(m, x, t, {"UNET_NO_POOL_FOLD": "1"}, seen2, split=True)
+    assert "splitk" in seen0 and "splitk" in seen1 and "splitk" in seen2, sorted(seen0)
+    assert "unet_conv:4" in seen0 and "unet_conv:4" not in seen1
+    assert "unet_bn_bwd_reduce_pool" in seen0 and "unet_bn_bwd_reduce_pool" not in seen2
+    assert torch.equal(out0, out1) and torch.equal(out0, out2)
+    diff = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+    assert not diff, diff
+    a = torch.cat([g0[n].double().flatten() for n in g0])
+    b = torch.cat([g2[n].double().flatten() for n in g0])
+    assert float((a - b).norm() / b.norm()) <= 1e-2
+    for n in g0:
+        if g0[n].numel() < 16:
+            continue    # a 1-channel BN's gamma / beta gradient (see test_outconv_bn_backward_fused)
+        d = float((g0[n].double() - g2[n].double()).abs().max() / (g2[n].double().abs().max() + 1e-30))
+        assert d <= 0.1, (n, d)
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
