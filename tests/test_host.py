@@ -159,3 +159,19 @@ def test_relu_after_16bit_rounding_identity(dt):
     # -0.0 (0x8000) in the reference is +0 in the new order
     ref_bits = torch.where(ref_bits == -32768, torch.zeros_like(ref_bits), ref_bits)
     assert torch.equal(new_bits, ref_bits)
+
+
+def test_torch_ops_library_registers_and_refuses_cpu():
+    """The TORCH_LIBRARY(unet_hip) operators (csrc/torch_ops.cpp) load on the host, report the header's ABI version,
+    carry the documented schemas, and refuse CPU tensors (no CPU kernels are registered; no fallback)."""
+    from unet._hip import lib as L
+    from unet._hip import torch_ops
+    ops = torch_ops.load()
+    assert ops.abi_version() == L.ABI_VERSION
+    assert "-> (Tensor loss, Tensor coef)" in str(ops.dice_bce_fwd.default._schema)
+    assert "int ignore_index=-1" in str(ops.confusion_matrix.default._schema)
+    z, t = torch.randn(1, 2, 8, 8), torch.zeros(1, 8, 8, dtype=torch.long)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        ops.dice_bce_fwd(z, t, 1.0, 1.0, 0.5, 1e-6, 1.0, True, 0)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        ops.confusion_matrix(z, t, 2)
