@@ -934,7 +934,10 @@ def test_pack_weights_batched_matches_single(prec):
     L, R = _lib(), _rt()
     P = R._PRECISIONS[prec]
     torch.manual_seed(21)
-    shapes = [(64, 64, 3), (40, 24, 3), (130, 64, 3), (32, 64, 1), (256, 512, 1), (1024, 512, 3), (64, 1, 3), (8, 33, 3)]
+    # round 6: 16-byte source loads for in-range tiles with 16-byte-aligned segments (Cin * taps % 4 == 0), the
+    # scalar path for the rest (partial tiles, Cin = 62 / 33 / 1), padded LDS layouts for both
+    shapes = [(64, 64, 3), (40, 24, 3), (130, 64, 3), (32, 64, 1), (256, 512, 1), (1024, 512, 3), (64, 1, 3), (8, 33, 3),
+              (128, 36, 3), (96, 62, 1), (256, 128, 1), (48, 128, 3)]
     jobs, outs, refs = [], [], []
     for co, ci, k in shapes:
         w = torch.randn(co, ci, k, k, device="cuda")
