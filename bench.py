@@ -344,7 +344,9 @@ def main():
     tfile = ROOT / "profiles" / "traffic.json"
     if tfile.exists():
         tr = json.loads(tfile.read_text())
-        ent = tr.get(f"{target}@{args.size}x{args.in_ch}") or tr.get(target)
+        # the un-suffixed key is the AttentionUNet headline's; a UNet line (C2) has its own "@unet" key or none
+        ent = tr.get(f"{target}@{args.size}x{args.in_ch}") or (
+            tr.get(target) if args.model == "attention_unet" else tr.get(f"{target}@unet"))
         traffic = ent.get("bytes_per_launch") if isinstance(ent, dict) else ent
     headline = (args.size, args.in_ch, args.accum, args.model) == (512, 1, 1, "attention_unet")
     metric = METRIC if headline else (
