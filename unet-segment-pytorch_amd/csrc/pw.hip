@@ -674,7 +674,12 @@ bool pw_wgrad_ok(const unet_wgrad_desc* d) {
   if ((d->dtype != UNET_BF16 && d->dtype != UNET_F16) || d->ksize != 1 || d->nsrc != 1 ||
       !pw_src_ok(d->src[0], d->Cin))
     return false;
-  if (d->Cin % 64 || d->Cout % 16 || P < 131072) return false;  // measured: wgrad2 wins at 128^2 x bs4
+  // smallest map served (pixels): wgrad2 won at 128^2 x bs4 when measured in round 4; UNET_PW_WGRAD_MINP re-tests it
+  static const long long minp = [] {
+    const char* e = getenv("UNET_PW_WGRAD_MINP");
+    return e && atoll(e) > 0 ? atoll(e) : 131072LL;
+  }();
+  if (d->Cin % 64 || d->Cout % 16 || P < minp) return false;
   return (double)P * d->Cin * 2 < (double)PW_OOB && (double)P * d->Cout * 2 < (double)PW_OOB;
 }
 
